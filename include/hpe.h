@@ -1,0 +1,161 @@
+/*
+ * include/hpe.h -- C ABI of the MI355X-native PSO / costfunc / handmodel hot path.
+ *
+ * Drop-in boundary for hjurong/hand-pose-estimation (reference paths below are
+ * /root/reference/src file:line).  Plain pointers and sizes only; no exceptions
+ * or C++ types cross it.  Every entry point returns 0 on success and a negative
+ * HPE_E* code on failure; hpe_last_error(ctx) returns the message.
+ *
+ * Conventions (matching the reference):
+ *   - theta: 26 doubles per particle, degrees for angles, cm for position
+ *     (handmodel.cpp:123-149); a batch is column-major 26 x P (PSO.cpp:67), i.e.
+ *     particle-contiguous, exactly Armadillo's mat::memptr() layout.
+ *   - sphere centres: 48 x 3 per particle, row-major here ([sphere][xyz]),
+ *     with y and z negated (handmodel.cpp:288).
+ *   - depth: 240 x 320 row-major ([v][u]); cm after preprocessing.
+ *   - cloud: N x 3 row-major (X, -Y, -Z) cm (observedmodel.cpp:157-161).
+ *   - match ids: int32 sphere index per cloud point (uvec matchId, costfunc.h:27).
+ *
+ * Ownership: the caller owns every host buffer; they are copied in/out and not
+ * retained after return.  The context owns all device memory and one HIP stream.
+ * Threading: one context per host thread per device; multi-GPU = one context per
+ * device.
+ */
+#ifndef HPE_H
+#define HPE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HPE_ABI_VERSION 1
+
+#define HPE_OK 0
+#define HPE_E_ARG -1      /* bad argument (null pointer, size out of range) */
+#define HPE_E_HIP -2      /* HIP runtime error */
+#define HPE_E_STATE -3    /* call order (e.g. no frame set, no PSO params) */
+#define HPE_E_NOMEM -4    /* allocation failed */
+#define HPE_E_NODEVICE -5 /* no gfx950 device visible */
+
+typedef struct hpe_ctx hpe_ctx;
+
+/* Hand geometry.  Replaces handmodel(h_geo, h_spacing, tb_spheres, fg_spheres,
+ * h_CMC, sphR) (handmodel.h:9-10, handmodel.cpp:10-27).  Sphere counts must be
+ * tb {2,2,2,2}, fg {4,2,2,2}: the reference hard-codes 8 + 4x10 rows
+ * (handmodel.cpp:272-286). */
+typedef struct {
+    double geo_cm[20];    /* misc/hgeo.dat / 10, thumb first (handmodel.cpp:107-121) */
+    double radii_cm[48];  /* misc/rad.dat / 10 (testmodel.cpp:49) */
+    double cmc_deg[5];    /* testmodel.cpp:37 */
+    double spacing_cm[5]; /* testmodel.cpp:36; narrowed to float like fingermodel.h:43 */
+    int32_t tb_spheres[4];
+    int32_t fg_spheres[4];
+} hpe_hand_params;
+
+/* Observation of one frame, already preprocessed (observedmodel getters,
+ * observedmodel.h:51-63 / observedmodel.cpp:383-409). */
+typedef struct {
+    const double *depth_cm; /* 240*320 */
+    const float *dt;        /* 240*320 distance transform of the background, px */
+    const double *cloud;    /* n*3 */
+    int32_t n;
+    double scale;           /* cm per pixel (get_img_scale) */
+    double dtmax;           /* max(dt) (costfunc.cpp:298) */
+    double K[9];            /* camera matrix row-major (get_camera_mat) */
+} hpe_frame;
+
+int hpe_abi_version(void);
+const char *hpe_last_error(const hpe_ctx *ctx);
+
+/* Context: device buffers, the hand constants and one stream on `device`. */
+int hpe_create(hpe_ctx **out, int device, const hpe_hand_params *hand);
+int hpe_destroy(hpe_ctx *ctx);
+/* hipStream_t of the context (for callers that order their own work after ours). */
+void *hpe_stream(hpe_ctx *ctx);
+int hpe_sync(hpe_ctx *ctx);
+
+/* observedmodel::init_observation / next_frame preprocessing on the host
+ * (observedmodel.cpp:110-219, 272-369): depth .bin (float mm, 240x320 row-major)
+ * -> depth cm, cloud (optionally down-sampled to 250), scale, distance transform.
+ * cloud_out capacity: 76800*3 doubles. */
+int hpe_preprocess_depth(const float *depth_mm, int to_cm, int downsample, double focal,
+                         double *depth_cm_out, float *dt_out, double *cloud_out,
+                         int32_t *n_out, double *scale_out, double *dtmax_out,
+                         double K_out[9]);
+
+/* Frame residency.  `slot` in [0, 4096): a frame stored once stays in HBM; select
+ * makes it the observation every following call uses (next_frame equivalent,
+ * observedmodel.cpp:420-430).  hpe_set_frame = store into slot 0 + select 0. */
+int hpe_store_frame(hpe_ctx *ctx, int slot, const hpe_frame *frame);
+int hpe_select_frame(hpe_ctx *ctx, int slot);
+int hpe_set_frame(hpe_ctx *ctx, const hpe_frame *frame);
+
+/* handmodel::build_hand_model for a batch (handmodel.cpp:259-298).
+ * theta: 26*P; S_out: P*48*3; joints_out (optional, may be NULL): P*21*3
+ * (hand_joints, handmodel.cpp:291-296). */
+int hpe_build_spheres(hpe_ctx *ctx, const double *theta, int P, double *S_out,
+                      double *joints_out);
+
+/* costfunc::cal_cost for a batch (costfunc.cpp:89-127; with_collision != 0 gives
+ * cal_cost2(theta, matchId, true) of costfunc.cpp:31-86).  Replaces the OpenMP
+ * particle loops of PSO.cpp:748-763 and :848-861.
+ * match_out (optional): P*n int32 correspondences (compute_correspondences). */
+int hpe_eval_costs(hpe_ctx *ctx, const double *theta, int P, int with_collision,
+                   double *cost_out, int32_t *match_out);
+
+/* costfunc::cal_cost2(theta, matchId, compute_corr, debug) (costfunc.cpp:31-86).
+ * match_inout: n int32; written when compute_corr != 0, read otherwise.
+ * terms_out (optional): {align, depth, collision}. */
+int hpe_cal_cost2(hpe_ctx *ctx, const double theta[26], int32_t *match_inout,
+                  int compute_corr, double *cost_out, double terms_out[3]);
+
+/* PSO::set_pso_params (PSO.cpp:38-54).  omega/phip/phig/minstep/minfunc are kept
+ * for API parity; pso_evolve uses the SPSO-2011 constants (PSO.cpp:772-774). */
+int hpe_set_pso_params(hpe_ctx *ctx, const double ub[26], const double lb[26],
+                       const double stdv[26], double omega, double phip, double phig,
+                       int maxiter, double minstep, double minfunc);
+/* The reference reseeds with 1000 on every pso_evolve (PSO.cpp:722). */
+int hpe_set_seed(hpe_ctx *ctx, uint64_t seed);
+
+/* PSO::pso_evolve(optfunc, x0, num_p, bestp) (PSO.cpp:717-886).
+ * bestcost_out (optional) = gbest cost (pbest cost of the gbest generation). */
+int hpe_pso_evolve(hpe_ctx *ctx, const double x0[26], int num_p, double bestp[26],
+                   double *bestcost_out);
+
+/* Per-generation trace of the last pso_evolve (debug / parity):
+ * gbest cost, stagnation count, topology generation; arrays of maxiter-1. */
+int hpe_pso_trace(hpe_ctx *ctx, double *gbest, int32_t *count, int32_t *topo, int n);
+
+/* PSO::refine_init_pose(x0, optfunc) (PSO.cpp:216-266).  evals_out optional. */
+int hpe_refine_init_pose(hpe_ctx *ctx, double x0[26], int32_t *evals_out);
+
+/* One tracked frame of test_full (testmodel.cpp:124-138) on the selected frame:
+ * [refine_init_pose] -> pso_evolve -> cost = cal_cost(bestp) -> x0 = bestp.
+ * x0_inout: 26 doubles (host).  cost_out optional. */
+int hpe_track_frame(hpe_ctx *ctx, int num_p, int refine, double x0_inout[26],
+                    double *cost_out);
+
+/* Same, device-resident: d_state is a device pointer to 27 doubles
+ * {x0[26], cost}; read as x0, overwritten with {bestp, cost}.  Asynchronous on
+ * hpe_stream(ctx): no host synchronisation. */
+int hpe_track_frame_dev(hpe_ctx *ctx, int num_p, int refine, double *d_state);
+
+/* Kernel timing with HIP events on the context stream (bench instrumentation).
+ * While enabled, every launch of the fused generation kernel (k_pso_gen) is
+ * bracketed by an event pair; hpe_profile_read synchronises and returns the count and
+ * total/min/max device milliseconds since the last enable. */
+int hpe_profile_enable(hpe_ctx *ctx, int on);
+int hpe_profile_read(hpe_ctx *ctx, int32_t *launches, double *total_ms, double *min_ms,
+                     double *max_ms);
+
+/* Synthetic 240x320 depth (float mm, zero background) of the 48-sphere model at
+ * pose theta: front-most ray/sphere hit per pixel centre under K(focal).  Bench /
+ * test input generator (no MSRA data on the box). */
+int hpe_render_depth(hpe_ctx *ctx, const double theta[26], double focal, float *depth_mm_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

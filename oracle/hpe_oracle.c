@@ -1,0 +1,697 @@
+/*
+ * oracle/hpe_oracle.c -- CPU restatement of the reference hot path.
+ * TEST INFRASTRUCTURE ONLY (see hpe_oracle.h for the parity status).
+ *
+ * Build: gcc -O2 -fopenmp -ffp-contract=off (oracle/Makefile).  No FMA
+ * contraction, left-to-right sums, reduction orders of Armadillo's
+ * accumulate/dot kernels where the reference goes through them.
+ */
+#include "hpe_oracle.h"
+
+#include <float.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+static const double ORA_PI = 3.141592653589793115997963468544185161590576171875; /* acos(-1) fingermodel.cpp:8 */
+
+/* fingermodel.cpp:203-205 / thumbmodel.cpp:220-222 */
+static double deg2rad(double a) { return a / 180.0 * ORA_PI; }
+
+/* row-major 4x4 product, k-ordered sums (Armadillo gemm_emul_tinysq order) */
+static void mm4(const double *A, const double *B, double *C) {
+    double T[16];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j)
+            T[i * 4 + j] = ((A[i * 4 + 0] * B[0 * 4 + j] + A[i * 4 + 1] * B[1 * 4 + j]) +
+                            A[i * 4 + 2] * B[2 * 4 + j]) +
+                           A[i * 4 + 3] * B[3 * 4 + j];
+    memcpy(C, T, sizeof(T));
+}
+
+static void set4(double *M, double a00, double a01, double a02, double a03, double a10,
+                 double a11, double a12, double a13, double a20, double a21, double a22,
+                 double a23) {
+    M[0] = a00; M[1] = a01; M[2] = a02; M[3] = a03;
+    M[4] = a10; M[5] = a11; M[6] = a12; M[7] = a13;
+    M[8] = a20; M[9] = a21; M[10] = a22; M[11] = a23;
+    M[12] = 0; M[13] = 0; M[14] = 0; M[15] = 1;
+}
+
+/* Fixed CMC transforms.  fingermodel.cpp:106-132 (T01, T10), thumbmodel.cpp:112-138
+ * (Trf, T10).  `spacing` is a float member (fingermodel.h:43, thumbmodel.h:42), so
+ * spacing*spacing is a float product. */
+void ora_hand_init(ora_hand *h, const double geo_cm[20], const double radii_cm[48],
+                   const double cmc_deg[5], const double spacing[5]) {
+    memcpy(h->geo, geo_cm, sizeof(h->geo));
+    memcpy(h->radii, radii_cm, sizeof(h->radii));
+    memcpy(h->cmc, cmc_deg, sizeof(h->cmc));
+    for (int d = 0; d < 5; ++d) h->spacing[d] = (float)spacing[d];
+    for (int d = 0; d < 5; ++d) {
+        const double L0 = h->geo[4 * d];
+        const float sp = h->spacing[d];
+        const double n = deg2rad(h->cmc[d]);
+        set4(h->F[d], cos(n), -sin(n), 0, L0 * cos(n), sin(n), cos(n), 0, L0 * sin(n), 0, 0,
+             1, 0);
+        const float sp2 = sp * sp;
+        const double a = sqrt(L0 * L0 + (double)sp2 - 2 * L0 * sp * cos(n));
+        const double beta = asin(sin(n) * sp / a);
+        if (d == 0) { /* thumb: thumbmodel.cpp:132-135 */
+            set4(h->T10[d], cos(beta), -sin(beta), 0, -a * cos(beta), sin(beta), cos(beta), 0,
+                 -a * sin(beta), 0, 0, 1, 0);
+        } else { /* finger: fingermodel.cpp:126-129 */
+            set4(h->T10[d], cos(beta), -sin(beta), 0, -L0 * sin(n) * cos(beta), sin(beta),
+                 cos(beta), 0, -L0 * sin(n) * sin(beta), 0, 0, 1, 0);
+        }
+    }
+}
+
+/* buildSpheres: fingermodel.cpp:208-267 (4 + 2 + 2 + 2), thumbmodel.cpp:227-274 (2x4) */
+static int build_spheres(const double J[15], int thumb, double *out /* rows x 3 */) {
+    int cnt = 0;
+    const int ns[4] = {thumb ? 2 : 4, 2, 2, 2};
+    for (int i = 0; i < 4; ++i) {
+        const double *a = J + 3 * i, *b = J + 3 * (i + 1);
+        if (i == 0 && !thumb) {
+            const double t = 1. / (ns[0] - 1);
+            for (int j = 0; j < ns[0]; ++j) {
+                const double wa = 1. - t * j, wb = t * j;
+                for (int c = 0; c < 3; ++c) out[3 * cnt + c] = wa * a[c] + wb * b[c];
+                ++cnt;
+            }
+        } else {
+            const double t = 1. / ns[i];
+            for (int j = 1; j < ns[i] + 1; ++j) {
+                const double wa = 1. - t * j, wb = t * j;
+                for (int c = 0; c < 3; ++c) out[3 * cnt + c] = wa * a[c] + wb * b[c];
+                ++cnt;
+            }
+        }
+    }
+    return cnt;
+}
+
+/* One digit.  fingermodel.cpp:70-182 + 270-317, thumbmodel.cpp:76-195 + 276-318.
+ * Chain {F, A*B, C3, C4} with joint0 = (cur*F*T10) taken at i == 1. */
+static void build_digit(const ora_hand *h, int d, const double th4[4], const double gb[3],
+                        const double gp[3], double J[15]) {
+    const double *g = h->geo + 4 * d;
+    const double a1 = deg2rad(th4[0]), a2 = deg2rad(th4[1]);
+    const double a3 = deg2rad(th4[2]), a4 = deg2rad(th4[3]);
+    const double TWS = deg2rad(gb[0] + 180), ANG = deg2rad(gb[1]), ROT = deg2rad(gb[2]);
+    double A[16], B[16], C3[16], C4[16], T00[16], Rz[16], Ry[16], Rx[16], Tgb[16];
+    /* A: finger T12 (fingermodel.cpp:137-140) == thumb T01 (thumbmodel.cpp:144-147) */
+    set4(A, cos(a1), 0, -sin(a1), 0, sin(a1), 0, cos(a1), 0, 0, -1, 0, 0);
+    if (d == 0) { /* thumb T12 with twist pCMC (thumbmodel.cpp:149-153) */
+        const double pc = deg2rad(h->cmc[0]) + ORA_PI;
+        set4(B, cos(a2), -sin(a2) * cos(pc), sin(a2) * sin(pc), g[1] * cos(a2), sin(a2),
+             cos(a2) * cos(pc), -cos(a2) * sin(pc), g[1] * sin(a2), 0, sin(pc), cos(pc), 0);
+    } else { /* finger T23 (fingermodel.cpp:142-145) */
+        set4(B, cos(a2), -sin(a2), 0, g[1] * cos(a2), sin(a2), cos(a2), 0, g[1] * sin(a2), 0,
+             0, 1, 0);
+    }
+    set4(C3, cos(a3), -sin(a3), 0, g[2] * cos(a3), sin(a3), cos(a3), 0, g[2] * sin(a3), 0, 0,
+         1, 0);
+    set4(C4, cos(a4), -sin(a4), 0, g[3] * cos(a4), sin(a4), cos(a4), 0, g[3] * sin(a4), 0, 0,
+         1, 0);
+    set4(T00, 1, 0, 0, gp[0], 0, 1, 0, gp[1], 0, 0, 1, gp[2]);
+    set4(Rz, cos(TWS), -sin(TWS), 0, 0, sin(TWS), cos(TWS), 0, 0, 0, 0, 1, 0);
+    set4(Ry, cos(ANG), 0, sin(ANG), 0, 0, 1, 0, 0, -sin(ANG), 0, cos(ANG), 0);
+    set4(Rx, 1, 0, 0, 0, 0, cos(ROT), -sin(ROT), 0, 0, sin(ROT), cos(ROT), 0);
+    mm4(Rz, Ry, Tgb);
+    mm4(Tgb, Rx, Tgb); /* Tgb = (Rz*Ry)*Rx, fingermodel.cpp:180 */
+    double AB[16];
+    mm4(A, B, AB); /* T123 = T12*T23 (fingermodel.cpp:287) / T012 = T01*T12 */
+    const double *chain[4] = {h->F[d], AB, C3, C4};
+    double cur[16];
+    mm4(T00, Tgb, cur);
+    for (int i = 0; i < 4; ++i) {
+        if (i == 1) {
+            double base[16];
+            mm4(cur, h->T10[d], base);
+            J[0] = base[3]; J[1] = base[7]; J[2] = base[11];
+        }
+        mm4(cur, chain[i], cur);
+        J[3 * (i + 1) + 0] = cur[3];
+        J[3 * (i + 1) + 1] = cur[7];
+        J[3 * (i + 1) + 2] = cur[11];
+    }
+}
+
+/* handmodel::build_hand_model, handmodel.cpp:259-298 (+ process_theta :123-149) */
+void ora_build_hand_model(const ora_hand *h, const double th[26], double S[144],
+                          double joints[63]) {
+    int row = 0;
+    double Jd[5][15];
+    for (int d = 0; d < 5; ++d) {
+        build_digit(h, d, th + 6 + 4 * d, th, th + 3, Jd[d]);
+        row += build_spheres(Jd[d], d == 0, S + 3 * row);
+    }
+    for (int i = 0; i < ORA_NS; ++i) { /* sphere_centres.cols(1,2) *= -1 (:288) */
+        S[3 * i + 1] *= -1;
+        S[3 * i + 2] *= -1;
+    }
+    if (joints) { /* hand_joints (:291-296): wrist, index..little rows 1-4, thumb rows 1-4 */
+        for (int c = 0; c < 3; ++c) joints[c] = th[3 + c];
+        const int order[5] = {1, 2, 3, 4, 0};
+        for (int k = 0; k < 5; ++k)
+            for (int r = 1; r < 5; ++r)
+                for (int c = 0; c < 3; ++c)
+                    joints[3 * (1 + 4 * k + (r - 1)) + c] = Jd[order[k]][3 * r + c];
+    }
+}
+
+/* compute_correspondences, costfunc.cpp:306-343: cv::BFMatcher(NORM_L2) on float32
+ * copies.  Per OpenCV 3.0 batchDistL2_32f: dist = sqrtf(((t0*t0) + t1*t1) + t2*t2)
+ * with t = q - train in float; K=1 keeps the first strictly-smaller distance,
+ * compared as int bit patterns (BatchDistInvoker), initial FLT_MAX / index -1. */
+void ora_correspondences(const ora_obs *o, const double S[144], int32_t *match) {
+    float sf[ORA_NS][3];
+    for (int j = 0; j < ORA_NS; ++j)
+        for (int c = 0; c < 3; ++c) sf[j][c] = (float)S[3 * j + c];
+    const float fmax_ = FLT_MAX;
+    int32_t fmax_bits;
+    memcpy(&fmax_bits, &fmax_, 4);
+    for (int i = 0; i < o->n; ++i) {
+        const float q0 = (float)o->cloud[3 * i], q1 = (float)o->cloud[3 * i + 1],
+                    q2 = (float)o->cloud[3 * i + 2];
+        int32_t best = fmax_bits, idx = -1;
+        for (int j = 0; j < ORA_NS; ++j) {
+            const float t0 = q0 - sf[j][0], t1 = q1 - sf[j][1], t2 = q2 - sf[j][2];
+            float d = 0.f;
+            d += t0 * t0;
+            d += t1 * t1;
+            d += t2 * t2;
+            const float s = sqrtf(d);
+            int32_t b;
+            memcpy(&b, &s, 4);
+            if (b < best) {
+                best = b;
+                idx = j;
+            }
+        }
+        match[i] = idx;
+    }
+}
+
+/* Armadillo arrayops::accumulate: two interleaved accumulators */
+static double accumulate2(const double *x, int n) {
+    double a1 = 0, a2 = 0;
+    int i, j;
+    for (i = 0, j = 1; j < n; i += 2, j += 2) {
+        a1 += x[i];
+        a2 += x[j];
+    }
+    if (i < n) a1 += x[i];
+    return a1 + a2;
+}
+
+/* op_dot::direct_dot_arma (n <= 32): two interleaved accumulators */
+static double dot2(const double *a, const double *b, int n) {
+    double v1 = 0, v2 = 0;
+    int i, j;
+    for (i = 0, j = 1; j < n; i += 2, j += 2) {
+        v1 += a[i] * b[i];
+        v2 += a[j] * b[j];
+    }
+    if (i < n) v1 += a[i] * b[i];
+    return v1 + v2;
+}
+
+/* align_models, costfunc.cpp:346-377 */
+double ora_align(const ora_hand *h, const ora_obs *o, const double S[144],
+                 const int32_t *match) {
+    double *dif = (double *)malloc(sizeof(double) * (o->n > 0 ? o->n : 1));
+    for (int i = 0; i < o->n; ++i) {
+        const int m = match[i];
+        const double dx = o->cloud[3 * i] - S[3 * m], dy = o->cloud[3 * i + 1] - S[3 * m + 1],
+                     dz = o->cloud[3 * i + 2] - S[3 * m + 2];
+        const double nd = sqrt((dx * dx + dy * dy) + dz * dz);
+        const double e = fabs(nd - h->radii[m]);
+        dif[i] = e * e;
+    }
+    const double lambda = (double)ORA_NS / (double)o->n;
+    const double r = accumulate2(dif, o->n) * lambda;
+    free(dif);
+    return r;
+}
+
+/* depth_penalty, costfunc.cpp:227-304.  Mutates S (un-negates y,z) like :249. */
+double ora_depth_penalty(const ora_hand *h, const ora_obs *o, double S[144]) {
+    const double *K = o->K;
+    double pen = 0.0;
+    for (int i = 0; i < ORA_NS; ++i) {
+        S[3 * i + 1] *= -1;
+        S[3 * i + 2] *= -1;
+    }
+    for (int i = 0; i < ORA_NS; ++i) {
+        const double x = S[3 * i], y = S[3 * i + 1], z = S[3 * i + 2];
+        const double pu = (K[0] * x + K[1] * y) + K[2] * z;
+        const double pv = (K[3] * x + K[4] * y) + K[5] * z;
+        const double pw = (K[6] * x + K[7] * y) + K[8] * z;
+        const double dx = floor(pu / pw), dy = floor(pv / pw);
+        const int xb = dx >= 0 && dx < ORA_W, yb = dy >= 0 && dy < ORA_H;
+        if (xb && yb) {
+            const int u = (int)dx, v = (int)dy;
+            const double djc = o->depth[v * ORA_W + u];
+            if (djc != 0.0) {
+                const double t = djc - z;
+                const double diff = (0.0 < t) ? t : 0.0; /* std::max(0.0, t) */
+                pen += diff * diff;
+            } else {
+                const double dd = (double)o->dt[v * ORA_W + u] * o->scale + h->radii[i];
+                pen += dd * dd;
+            }
+        } else {
+            const double md = o->dtmax * o->scale + h->radii[i];
+            pen += md * md;
+        }
+    }
+    return pen;
+}
+
+/* self_collision_penalty, costfunc.cpp:130-197: 4 adjacent digit pairs, rows
+ * {2..7, 12..17, 22..27, 32..37, 42..47}; pair k = (a = k/6, b = k%6). */
+double ora_collision(const ora_hand *h, const double S[144]) {
+    const int base[5] = {2, 12, 22, 32, 42};
+    double pen = 0.0;
+    for (int p = 0; p < 4; ++p) {
+        double pos[36];
+        int np = 0;
+        for (int k = 0; k < 36; ++k) {
+            const int a = base[p] + k / 6, b = base[p + 1] + k % 6;
+            const double dx = S[3 * b] - S[3 * a], dy = S[3 * b + 1] - S[3 * a + 1],
+                         dz = S[3 * b + 2] - S[3 * a + 2];
+            const double dist = sqrt((dx * dx + dy * dy) + dz * dz);
+            const double v = (h->radii[b] + h->radii[a]) - dist;
+            if (v > 0) pos[np++] = v * v;
+        }
+        pen += accumulate2(pos, np);
+    }
+    return pen;
+}
+
+/* cal_cost, costfunc.cpp:89-127 (no collision term, :122) */
+double ora_cal_cost(const ora_hand *h, const ora_obs *o, const double th[26]) {
+    double S[144];
+    ora_build_hand_model(h, th, S, NULL);
+    int32_t *m = (int32_t *)malloc(sizeof(int32_t) * (o->n > 0 ? o->n : 1));
+    ora_correspondences(o, S, m);
+    const double a = ora_align(h, o, S, m);
+    const double d = ora_depth_penalty(h, o, S);
+    free(m);
+    return a + d;
+}
+
+/* cal_cost2, costfunc.cpp:31-86 */
+double ora_cal_cost2(const ora_hand *h, const ora_obs *o, const double th[26],
+                     int32_t *match, int compute_corr, double terms[3]) {
+    double S[144];
+    ora_build_hand_model(h, th, S, NULL);
+    if (compute_corr) ora_correspondences(o, S, match);
+    const double a = ora_align(h, o, S, match);
+    const double d = ora_depth_penalty(h, o, S); /* mutates S, as the reference */
+    const double c = ora_collision(h, S);
+    if (terms) {
+        terms[0] = a;
+        terms[1] = d;
+        terms[2] = c;
+    }
+    return a + d + c;
+}
+
+void ora_eval_costs(const ora_hand *h, const ora_obs *o, const double *thetas, int P,
+                    int with_collision, double *cost, int nthreads) {
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
+#endif
+    for (int i = 0; i < P; ++i) {
+        if (with_collision) {
+            int32_t *m = (int32_t *)malloc(sizeof(int32_t) * (o->n > 0 ? o->n : 1));
+            cost[i] = ora_cal_cost2(h, o, thetas + 26 * i, m, 1, NULL);
+            free(m);
+        } else {
+            cost[i] = ora_cal_cost(h, o, thetas + 26 * i);
+        }
+    }
+}
+
+/* ---------------- Philox4x32-10 (Salmon et al., SC'11) ---------------- */
+void ora_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+    uint32_t k0 = key[0], k1 = key[1];
+    for (int r = 0; r < 10; ++r) {
+        if (r > 0) {
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+double ora_u01(uint64_t seed, uint32_t stream, uint32_t gen, uint32_t idx, uint32_t k) {
+    const uint32_t ctr[4] = {k >> 1, idx, gen, stream};
+    const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t out[4];
+    ora_philox4x32_10(ctr, key, out);
+    const int p = (int)(k & 1u) * 2;
+    const uint64_t u53 = ((uint64_t)out[p] << 21) | (out[p + 1] >> 11);
+    return (double)u53 * 0x1.0p-53;
+}
+
+enum { ST_NORMAL = 1, ST_RP = 2, ST_RG = 3, ST_LINK = 4 };
+
+/* randn<mat>(26, P) replacement: Box-Muller on Philox pairs (dims 2q, 2q+1) */
+void ora_normals(uint64_t seed, int P, double *out) {
+    for (int i = 0; i < P; ++i)
+        for (int q = 0; q < ORA_DOF / 2; ++q) {
+            const double u1 = ora_u01(seed, ST_NORMAL, 0, (uint32_t)i, 2u * q);
+            const double u2 = ora_u01(seed, ST_NORMAL, 0, (uint32_t)i, 2u * q + 1);
+            const double r = sqrt(-2.0 * log(1.0 - u1));
+            const double t = 6.283185307179586231995926937088370323181152343750 * u2;
+            out[ORA_DOF * i + 2 * q] = r * cos(t);
+            out[ORA_DOF * i + 2 * q + 1] = r * sin(t);
+        }
+}
+
+/* check_constraints, PSO.cpp:358-377 (above-max clamps to MIN, :372) */
+static void check_constraints(double *x, double *v, const double *lb, const double *ub) {
+    for (int d = 0; d < ORA_DOF; ++d) {
+        const double xo = x[d];
+        if (xo < lb[d]) {
+            x[d] = lb[d];
+            v[d] = 0.;
+        }
+        if (xo > ub[d]) {
+            x[d] = lb[d];
+            v[d] = 0.;
+        }
+    }
+}
+
+/* pso_evolve, PSO.cpp:717-886 */
+int ora_pso_evolve(const ora_hand *h, const ora_obs *o, const double x0[26], int P,
+                   int maxiter, const double lb[26], const double ub[26],
+                   const double stdv[26], uint64_t seed, double bestp[26],
+                   double *bestcost, ora_pso_trace *trace, int nthreads) {
+    const int D = ORA_DOF;
+    double *x = (double *)calloc((size_t)D * P, sizeof(double));
+    double *v = (double *)calloc((size_t)D * P, sizeof(double));
+    double *pb = (double *)calloc((size_t)D * P, sizeof(double));
+    double *pc = (double *)calloc((size_t)P, sizeof(double));
+    double *fx = (double *)calloc((size_t)P, sizeof(double));
+    int *links = (int *)calloc((size_t)3 * P, sizeof(int));
+    int *in_off = (int *)calloc((size_t)P + 1, sizeof(int));
+    int *in_src = (int *)calloc((size_t)3 * P, sizeof(int));
+    int *fill = (int *)calloc((size_t)P, sizeof(int));
+    double gpos[26], gcost = 1e100;
+    memset(gpos, 0, sizeof(gpos));
+
+    /* generate_particles, PSO.cpp:56-74 */
+    ora_normals(seed, P, x);
+    for (int i = 0; i < P; ++i)
+        for (int d = 0; d < D; ++d) x[D * i + d] = x0[d] + x[D * i + d] * stdv[d];
+    memcpy(pb, x, sizeof(double) * D * P);
+    ora_eval_costs(h, o, x, P, 0, pc, nthreads); /* PSO.cpp:748-763 */
+    if (trace && trace->pcost0) memcpy(trace->pcost0, pc, sizeof(double) * P);
+    for (int i = 0; i < P; ++i) /* serial semantics of the racy init update */
+        if (pc[i] < gcost) {
+            gcost = pc[i];
+            memcpy(gpos, x + D * i, sizeof(gpos));
+        }
+
+    const double W1 = 1. / (2 * log(2.0)), C1 = 0.5 + log(2.0), C2 = C1; /* :772-774 */
+    int count = 100, topo = -1;
+    for (int g = 1; g < maxiter; ++g) { /* iter 2..maxiter, :778-780 */
+        if (count > 0) { /* topology rebuild, :790-803 */
+            for (int s = 0; s < P; ++s)
+                for (int k = 0; k < 3; ++k) {
+                    const double u = ora_u01(seed, ST_LINK, (uint32_t)g, (uint32_t)s, (uint32_t)k);
+                    links[3 * s + k] = (int)floor(u * (P - 1) + 0.5);
+                }
+            memset(in_off, 0, sizeof(int) * (P + 1));
+            for (int e = 0; e < 3 * P; ++e) in_off[links[e] + 1]++;
+            for (int i = 0; i < P; ++i) in_off[i + 1] += in_off[i];
+            memset(fill, 0, sizeof(int) * P);
+            for (int s = 0; s < P; ++s) /* ascending source order */
+                for (int k = 0; k < 3; ++k) {
+                    const int r = links[3 * s + k];
+                    in_src[in_off[r] + fill[r]++] = s;
+                }
+            topo = g;
+        }
+        for (int i = 0; i < P; ++i) { /* serial velocity loop, :807-845 */
+            /* informant = first argmin of pcost over find(L.col(i)==1) (:810-812):
+             * candidates are {i} U incoming, lowest index wins ties */
+            int inf = -1;
+            double best = 0;
+            int lo = in_off[i], hi = in_off[i + 1], e = lo;
+            int self_done = 0;
+            for (;;) { /* merge self into the ascending incoming list */
+                int s;
+                if (!self_done && (e >= hi || i <= in_src[e])) {
+                    s = i;
+                    self_done = 1;
+                } else if (e < hi) {
+                    s = in_src[e++];
+                } else
+                    break;
+                if (inf < 0 || pc[s] < best) {
+                    best = pc[s];
+                    inf = s;
+                }
+            }
+            double *xi = x + D * i, *vi = v + D * i;
+            const double *pbi = pb + D * i, *pbn = pb + D * inf;
+            for (int d = 0; d < D; ++d) {
+                const double rp = ora_u01(seed, ST_RP, (uint32_t)g, (uint32_t)i, (uint32_t)d);
+                const double rg = ora_u01(seed, ST_RG, (uint32_t)g, (uint32_t)i, (uint32_t)d);
+                if (inf == i)
+                    vi[d] = W1 * vi[d] + (C1 * rp) * (pbi[d] - xi[d]);
+                else
+                    vi[d] = (W1 * vi[d] + (C1 * rp) * (pbi[d] - xi[d])) +
+                            (C2 * rg) * (pbn[d] - xi[d]);
+            }
+            for (int d = 0; d < D; ++d) xi[d] = xi[d] + vi[d];
+            check_constraints(xi, vi, lb, ub);
+        }
+        ora_eval_costs(h, o, x, P, 0, fx, nthreads); /* :848-861 */
+        for (int i = 0; i < P; ++i)
+            if (fx[i] < pc[i]) {
+                pc[i] = fx[i];
+                memcpy(pb + D * i, x + D * i, sizeof(double) * D);
+            }
+        int fid = 0; /* pcost.min(fmin_id): first minimum, :864-865 */
+        for (int i = 1; i < P; ++i)
+            if (pc[i] < pc[fid]) fid = i;
+        const double fmin = pc[fid];
+        if (fmin < gcost) { /* gbest = particles.col(fmin_id), :869-873 */
+            memcpy(gpos, x + D * fid, sizeof(gpos));
+            gcost = fmin;
+            count = 0;
+        } else
+            count += 1;
+        if (trace) {
+            if (trace->gbest_trace) trace->gbest_trace[g - 1] = gcost;
+            if (trace->fmin_trace) trace->fmin_trace[g - 1] = fmin;
+            if (trace->count_trace) trace->count_trace[g - 1] = count;
+            if (trace->topo_trace) trace->topo_trace[g - 1] = topo;
+        }
+    }
+    memcpy(bestp, gpos, sizeof(gpos));
+    if (bestcost) *bestcost = gcost;
+    free(x); free(v); free(pb); free(pc); free(fx);
+    free(links); free(in_off); free(in_src); free(fill);
+    return 1;
+}
+
+/* goldstein, PSO.cpp:438-480 */
+static double goldstein(const ora_hand *h, const ora_obs *o, const double *theta,
+                        const double *g, int32_t *match, double fk, int maxiter, int *evals) {
+    double a = 0, b = 1e100, alpha = 0.5;
+    const double t = 2, c = 0.25;
+    double p[26], th1[26];
+    for (int d = 0; d < 26; ++d) p[d] = -1 * g[d];
+    for (int it = 0; it < maxiter; ++it) {
+        for (int d = 0; d < 26; ++d) th1[d] = theta[d] + alpha * p[d];
+        const double f1 = ora_cal_cost2(h, o, th1, match, 0, NULL);
+        ++*evals;
+        const double gp = dot2(g, p, 26);
+        const double armijo = fk + c * alpha * gp;
+        const double gold = fk + (1 - c) * alpha * gp;
+        if (f1 <= armijo) {
+            if (f1 >= gold) return alpha;
+            a = alpha;
+            const double up = t * alpha, mid = 0.5 * (alpha + b);
+            alpha = (mid < up) ? mid : up; /* std::min */
+        } else {
+            b = alpha;
+            alpha = 0.5 * (a + alpha);
+        }
+    }
+    return 0;
+}
+
+/* refine_init_pose + cal_grad, PSO.cpp:183-266.  Returns number of cost evals. */
+int ora_refine_init_pose(const ora_hand *h, const ora_obs *o, double x0[26]) {
+    const int start_idx[2] = {0, 3}, end_idx[2] = {2, 5};
+    int32_t *match = (int32_t *)malloc(sizeof(int32_t) * (o->n > 0 ? o->n : 1));
+    int evals = 0;
+    for (int blk = 0; blk < 2; ++blk) {
+        const double eps = 1e-6;
+        double tol = 1;
+        int cnt = 0, iter = 0;
+        const int maxiter = 15;
+        while (tol > eps && iter < maxiter && cnt < 1) {
+            const double fk = ora_cal_cost2(h, o, x0, match, 1, NULL);
+            evals++;
+            double grad[26];
+            for (int i = 0; i < 26; ++i) {
+                grad[i] = 0;
+                if (i >= start_idx[blk] && i <= end_idx[blk]) {
+                    const double e = 1e-5;
+                    double xph[26], xmh[26];
+                    memcpy(xph, x0, sizeof(xph));
+                    memcpy(xmh, x0, sizeof(xmh));
+                    xph[i] += e;
+                    xmh[i] -= e;
+                    const double fp = ora_cal_cost2(h, o, xph, match, 0, NULL);
+                    const double fm = ora_cal_cost2(h, o, xmh, match, 0, NULL);
+                    evals += 2;
+                    grad[i] = (fp - fm) / (2 * e);
+                }
+            }
+            const double tk = goldstein(h, o, x0, grad, match, fk, 30, &evals);
+            if (tk == 0) cnt += 1;
+            for (int d = 0; d < 26; ++d) x0[d] = x0[d] - tk * grad[d];
+            double g2[26];
+            for (int d = 0; d < 26; ++d) g2[d] = grad[d] * grad[d];
+            tol = sqrt(accumulate2(g2, 26));
+            iter += 1;
+        }
+    }
+    free(match);
+    return evals;
+}
+
+/* ---------------- observation preprocessing ---------------- */
+
+/* invert_depthmap + cv::distanceTransform(CV_DIST_L2, 5), observedmodel.cpp:313-358.
+ * OpenCV 3.0 distanceTransform_5x5: 16.16 fixed point, metrics {1, 1.4f, 2.1969f}
+ * (CV_FLT_TO_FIX = cvRound(float*65536)), border INIT_DIST0 = INT_MAX >> 2,
+ * output (float)(t * (1.f/65536)).  Recalled OpenCV source: parity unpinned. */
+void ora_dist_transform(const double *depth_cm, float *dt_out) {
+    const unsigned HV = 65536u, DIAG = 91750u, LONG = 143976u;
+    const unsigned INIT = 0x7FFFFFFFu >> 2;
+    const int B = 2, W = ORA_W, H = ORA_H, ST = W + 2 * B;
+    unsigned *tmp = (unsigned *)malloc(sizeof(unsigned) * ST * (H + 2 * B));
+    for (int i = 0; i < ST * (H + 2 * B); ++i) tmp[i] = INIT;
+#define T(r, c) tmp[((r) + B) * ST + (c) + B]
+    for (int i = 0; i < H; ++i)
+        for (int j = 0; j < W; ++j) {
+            if (depth_cm[i * W + j] != 0) { /* inverted: hand pixel -> 0 */
+                T(i, j) = 0;
+                continue;
+            }
+            unsigned t0 = T(i - 2, j - 1) + LONG, t;
+            t = T(i - 2, j + 1) + LONG; if (t0 > t) t0 = t;
+            t = T(i - 1, j - 2) + LONG; if (t0 > t) t0 = t;
+            t = T(i - 1, j - 1) + DIAG; if (t0 > t) t0 = t;
+            t = T(i - 1, j) + HV;       if (t0 > t) t0 = t;
+            t = T(i - 1, j + 1) + DIAG; if (t0 > t) t0 = t;
+            t = T(i - 1, j + 2) + LONG; if (t0 > t) t0 = t;
+            t = T(i, j - 1) + HV;       if (t0 > t) t0 = t;
+            T(i, j) = t0;
+        }
+    const float scale = 1.f / 65536;
+    for (int i = H - 1; i >= 0; --i)
+        for (int j = W - 1; j >= 0; --j) {
+            unsigned t0 = T(i, j);
+            if (t0 > HV) {
+                unsigned t;
+                t = T(i + 2, j + 1) + LONG; if (t0 > t) t0 = t;
+                t = T(i + 2, j - 1) + LONG; if (t0 > t) t0 = t;
+                t = T(i + 1, j + 2) + LONG; if (t0 > t) t0 = t;
+                t = T(i + 1, j + 1) + DIAG; if (t0 > t) t0 = t;
+                t = T(i + 1, j) + HV;       if (t0 > t) t0 = t;
+                t = T(i + 1, j - 1) + DIAG; if (t0 > t) t0 = t;
+                t = T(i + 1, j - 2) + LONG; if (t0 > t) t0 = t;
+                t = T(i, j + 1) + HV;       if (t0 > t) t0 = t;
+                T(i, j) = t0;
+            }
+            dt_out[i * W + j] = (float)t0 * scale;
+        }
+#undef T
+    free(tmp);
+}
+
+/* load_data + depth_to_ptncloud + dist_transform, observedmodel.cpp:110-219,272-369.
+ * imgW=240, imgH=320 naming as testmodel.cpp:62; K = [[f,0,160],[0,f,120],[0,0,1]]. */
+int ora_preprocess(const float *depth_mm, int to_cm, int downsample, double focal,
+                   double *depth_cm_out, float *dt_out, double *cloud_out, int *n_out,
+                   double *scale_out, double *dtmax_out, double K_out[9]) {
+    const int W = ORA_W, H = ORA_H;
+    const double cx = 320 / 2., cy = 240 / 2.;
+    const double K[9] = {focal, 0.0, cx, 0.0, focal, cy, 0.0, 0.0, 1.0};
+    memcpy(K_out, K, sizeof(K));
+    for (int i = 0; i < W * H; ++i)
+        depth_cm_out[i] = to_cm ? (double)depth_mm[i] / 10. : (double)depth_mm[i];
+    int n = 0;
+    double sum1 = 0, sum2 = 0; /* accumulate2 over cmPerPixel, streamed */
+    int ncm = 0;
+    for (int r = 0; r < H; ++r)
+        for (int c = 0; c < W; ++c) {
+            const double Z = depth_cm_out[r * W + c];
+            if (Z == 0) continue;
+            const double X = ((c - cx) * Z) / focal, Y = ((r - cy) * Z) / focal;
+            cloud_out[3 * n] = X;
+            cloud_out[3 * n + 1] = Y * -1;
+            cloud_out[3 * n + 2] = Z * -1;
+            ++n;
+            /* scale: project (X,Y,Z) and (X+2,Y,Z), :171-202 */
+            const double pu = (K[0] * X + K[1] * Y) + K[2] * Z, pw = (K[6] * X + K[7] * Y) + K[8] * Z;
+            const double pv = (K[3] * X + K[4] * Y) + K[5] * Z;
+            const double Xe = X + 2.0;
+            const double eu = (K[0] * Xe + K[1] * Y) + K[2] * Z, ew = (K[6] * Xe + K[7] * Y) + K[8] * Z;
+            const double ev = (K[3] * Xe + K[4] * Y) + K[5] * Z;
+            const double du = floor(eu / ew) - floor(pu / pw), dv = floor(ev / ew) - floor(pv / pw);
+            const double dn = sqrt(du * du + dv * dv);
+            if (dn != 0) {
+                const double cm = 2.0 / dn;
+                if (ncm & 1) sum2 += cm; else sum1 += cm;
+                ++ncm;
+            }
+        }
+    *scale_out = ncm ? (sum1 + sum2) / ncm : NAN;
+    if (downsample) { /* :204-217, sample_f = N / 250 (degenerate when N < 250) */
+        const int ns = 250, f = n / ns;
+        for (int k = 0; k < ns; ++k) {
+            const int src = k * f;
+            double p0 = cloud_out[3 * src], p1 = cloud_out[3 * src + 1], p2 = cloud_out[3 * src + 2];
+            cloud_out[3 * k] = p0;
+            cloud_out[3 * k + 1] = p1;
+            cloud_out[3 * k + 2] = p2;
+        }
+        if (n == 0) {
+            for (int k = 0; k < ns * 3; ++k) cloud_out[k] = 0; /* reference reads row 0 of an empty mat: UB */
+        }
+        n = ns;
+    }
+    *n_out = n;
+    ora_dist_transform(depth_cm_out, dt_out);
+    float mx = dt_out[0];
+    for (int i = 1; i < W * H; ++i)
+        if (dt_out[i] > mx) mx = dt_out[i];
+    *dtmax_out = (double)mx;
+    return 0;
+}

@@ -1,0 +1,240 @@
+"""GPU parity: the HIP path (through the C ABI) against the C oracle on identical inputs.
+
+Tolerances (north_star: "within a stated float tolerance"):
+  * sphere centres / joints: |diff| <= 1e-9 cm (fp64 FK; only libm vs ocml sin/cos
+    rounding can differ)
+  * correspondences: identical, except a point whose two nearest float distances lie
+    within 1 ulp of each other (FK rounding may move a float centre by 1 ulp); such
+    points must still be matched to an equidistant sphere (tie-aware comparator)
+  * costs: relative 1e-9 (fp64 accumulation order differs: tree vs Armadillo's
+    2-accumulator sum)
+  * PSO / refine / tracking: bestp |diff| <= 1e-6, cost relative 1e-8
+"""
+import numpy as np
+import pytest
+
+import hand_data
+import oracle_np
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-9
+
+
+@pytest.fixture(scope="module")
+def hpe_mod():
+    import hpe
+    return hpe
+
+
+@pytest.fixture(scope="module")
+def gpu_hand(hpe_mod):
+    return hpe_mod.reference_hand(device=0)
+
+
+def _frame(np_hand, theta, downsample=True):
+    return oracle_np.render_depth_mm(np_hand, theta)
+
+
+def _obs_pair(oracle, gpu_hand, depth_mm, downsample=True):
+    import hpe
+    obs = oracle.preprocess(depth_mm, downsample=downsample)
+    om = hpe.observedmodel()
+    om.to_cm, om.downsample, om.focal_len = True, downsample, 241.42
+    om.set_depth_mm(depth_mm)
+    return obs, om
+
+
+def _match_equiv(obs, S, m_gpu, m_ref):
+    """Tie-aware: a differing match must be (float-)equidistant to the reference one."""
+    diff = np.nonzero(m_gpu != m_ref)[0]
+    if len(diff) == 0:
+        return True
+    q = obs.cloud[diff].astype(np.float32)
+    s = S.astype(np.float32)
+    d_g = np.linalg.norm(q - s[m_gpu[diff]], axis=1)
+    d_r = np.linalg.norm(q - s[m_ref[diff]], axis=1)
+    return bool(np.all(np.abs(d_g - d_r) <= 4 * np.spacing(np.maximum(d_g, d_r))))
+
+
+def test_render_matches_numpy(gpu_hand, np_hand):
+    th = oracle_np.X0
+    d_gpu = gpu_hand.ctx.render_depth(th)
+    d_np = oracle_np.render_depth_mm(np_hand, th)
+    assert ((d_gpu > 0) == (d_np > 0)).mean() > 0.9995
+    both = (d_gpu > 0) & (d_np > 0)
+    assert np.abs(d_gpu[both] - d_np[both]).max() < 1e-3
+
+
+def test_preprocess_host_matches_oracle(oracle, np_hand):
+    import hpe
+    d = oracle_np.render_depth_mm(np_hand, oracle_np.X0)
+    for ds in (True, False):
+        a = hpe.preprocess_depth(d, downsample=ds)
+        b = oracle.preprocess(d, downsample=ds)
+        np.testing.assert_array_equal(a["cloud"], b.cloud)
+        np.testing.assert_array_equal(a["dt"], b.dt)
+        np.testing.assert_array_equal(a["depth_cm"], b.depth)
+        assert a["scale"] == b.scale and a["dtmax"] == b.dtmax
+
+
+def test_fk_spheres_and_joints(oracle, ora_hand, gpu_hand):
+    rng = np.random.default_rng(1)
+    th = np.vstack([oracle_np.X0, hand_data.random_thetas(rng, 63, spread=3.0)])
+    th[5] = 0.0
+    th[6, 0:3] = (180.0, -180.0, 90.0)
+    S, J = gpu_hand.build_batch(th)
+    for i in range(len(th)):
+        Sr, Jr = oracle.build(ora_hand, th[i], joints=True)
+        np.testing.assert_allclose(S[i], Sr, rtol=0, atol=1e-9)
+        np.testing.assert_allclose(J[i], Jr, rtol=0, atol=1e-9)
+
+
+@pytest.mark.parametrize("downsample", [True, False])
+def test_eval_costs_and_matches(oracle, ora_hand, gpu_hand, np_hand, downsample):
+    import hpe
+    rng = np.random.default_rng(2)
+    truth = hand_data.trajectory(3, seed=5)[2]
+    d = oracle_np.render_depth_mm(np_hand, truth)
+    obs, om = _obs_pair(oracle, gpu_hand, d, downsample)
+    cf = hpe.costfunc(gpu_hand, om)
+    P = 48 if downsample else 12
+    th = hand_data.random_thetas(rng, P, x0=truth, spread=0.4)
+    th[0] = truth
+    cost, match = cf.cal_cost_batch(th, return_match=True)
+    ref = oracle.eval_costs(ora_hand, obs, th)
+    np.testing.assert_allclose(cost, ref, rtol=RTOL, atol=0)
+    for i in range(P):
+        S = oracle.build(ora_hand, th[i])
+        mr = oracle.correspondences(obs, S)
+        assert _match_equiv(obs, S, match[i], mr)
+    cost2 = cf.cal_cost_batch(th, with_collision=True)
+    ref2 = oracle.eval_costs(ora_hand, obs, th, with_collision=True)
+    np.testing.assert_allclose(cost2, ref2, rtol=RTOL, atol=0)
+
+
+def test_cal_cost2_terms_and_frozen(oracle, ora_hand, gpu_hand, np_hand):
+    import hpe
+    d = oracle_np.render_depth_mm(np_hand, oracle_np.X0)
+    obs, om = _obs_pair(oracle, gpu_hand, d)
+    cf = hpe.costfunc(gpu_hand, om)
+    th = oracle_np.X0 + 2.0
+    m = np.zeros(obs.n, dtype=np.int32)
+    c = cf.cal_cost2(th, m, True)
+    cr, tr, mr = oracle.terms(ora_hand, obs, th)
+    assert abs(c - cr) <= RTOL * abs(cr)
+    np.testing.assert_allclose(cf.last_terms, tr, rtol=RTOL, atol=1e-300)
+    assert np.array_equal(m, mr)
+    th2 = th.copy(); th2[0] += 1e-5
+    c2 = cf.cal_cost2(th2, m, False)
+    cr2, tr2, _ = oracle.terms(ora_hand, obs, th2, match=mr)
+    assert abs(c2 - cr2) <= RTOL * abs(cr2)
+
+
+def test_match_ties_lowest_index(oracle, ora_hand, gpu_hand):
+    """Cloud points placed exactly on float midpoints of sphere pairs: BFMatcher keeps
+    the first of equal distances (and equal sqrtf values)."""
+    import hpe
+    th = oracle_np.X0
+    S = oracle.build(ora_hand, th).astype(np.float32).astype(np.float64)
+    rng = np.random.default_rng(3)
+    pts = []
+    for _ in range(400):
+        a, b = rng.choice(48, 2, replace=False)
+        pts.append(0.5 * (S[a] + S[b]))
+    pts += list(S)  # exact centres: distance 0
+    cloud = np.array(pts)
+    depth = np.zeros((240, 320)); dt = np.zeros((240, 320), np.float32)
+    K = np.array([[241.42, 0, 160], [0, 241.42, 120], [0, 0, 1.0]])
+    import oracle_c
+    obs = oracle_c.Obs(depth, dt, cloud, 0.1, 0.0, K)
+    gpu_hand.ctx.store_frame(3, depth, dt, cloud, 0.1, 0.0, K)
+    gpu_hand.ctx.select_frame(3)
+    gpu_hand.ctx.frame_token = None
+    om = hpe.observedmodel(); om._obs = dict(cloud=cloud); om.token = -1
+    cf = hpe.costfunc(gpu_hand, om)
+    cf._sync_frame = lambda: None
+    cost, match = cf.cal_cost_batch(th[None, :], return_match=True)
+    mr = oracle.correspondences(obs, oracle.build(ora_hand, th))
+    assert np.array_equal(match[0], mr)
+    assert abs(cost[0] - oracle.cal_cost(ora_hand, obs, th)) <= RTOL * abs(cost[0])
+
+
+@pytest.mark.parametrize("P,maxiter", [(32, 11), (7, 4), (1, 3), (64, 1)])
+def test_pso_evolve(oracle, ora_hand, gpu_hand, np_hand, P, maxiter):
+    import hpe
+    truth = hand_data.trajectory(2, seed=9)[1]
+    d = oracle_np.render_depth_mm(np_hand, truth)
+    obs, om = _obs_pair(oracle, gpu_hand, d)
+    cf = hpe.costfunc(gpu_hand, om)
+    ub, lb, sd = oracle_np.reference_bounds()
+    pso = hpe.PSO()
+    pso.set_pso_params(ub, lb, sd, 0.7298, 1.49618, 1.49618, maxiter, 1e-8, 1e-8)
+    bestp = np.zeros(26)
+    x0 = oracle_np.X0.copy()
+    assert pso.pso_evolve(cf, x0, P, bestp) == 1
+    rb, rc, tr = oracle.pso_evolve(ora_hand, obs, x0, P, maxiter, lb, ub, sd, seed=1000)
+    np.testing.assert_allclose(bestp, rb, rtol=0, atol=1e-6)
+    assert abs(pso.last_gbest_cost - rc) <= 1e-8 * abs(rc)
+    if maxiter > 1:
+        g, cnt, topo = pso.trace(cf)
+        np.testing.assert_allclose(g, tr["gbest"], rtol=1e-8)
+        assert np.array_equal(cnt, tr["count"])
+        assert np.array_equal(topo, tr["topo"])
+
+
+def test_refine_init_pose(oracle, ora_hand, gpu_hand, np_hand):
+    import hpe
+    truth = hand_data.trajectory(2, seed=4)[1]
+    d = oracle_np.render_depth_mm(np_hand, truth)
+    obs, om = _obs_pair(oracle, gpu_hand, d)
+    cf = hpe.costfunc(gpu_hand, om)
+    x0 = oracle_np.X0.copy()
+    x_ref, ev_ref = oracle.refine(ora_hand, obs, x0)
+    pso = hpe.PSO()
+    x = x0.copy()
+    pso.refine_init_pose(x, cf)
+    assert pso.last_refine_evals == ev_ref
+    np.testing.assert_allclose(x, x_ref, rtol=0, atol=1e-6)
+
+
+def test_track_sequence(oracle, ora_hand, gpu_hand, np_hand):
+    """test_full's loop (testmodel.cpp:117-139) on 3 synthetic frames, 32 particles."""
+    import hpe
+    poses = hand_data.trajectory(3, seed=11)
+    ub, lb, sd = oracle_np.reference_bounds()
+    pso = hpe.PSO()
+    pso.set_pso_params(ub, lb, sd, 0.7298, 1.49618, 1.49618, 6, 1e-8, 1e-8)
+    x_gpu = oracle_np.X0.copy(); x_ref = oracle_np.X0.copy()
+    om = hpe.observedmodel(); om.downsample = True
+    cf = hpe.costfunc(gpu_hand, om)
+    for f in range(3):
+        d = oracle_np.render_depth_mm(np_hand, poses[f])
+        om.set_depth_mm(d)
+        obs = oracle.preprocess(d)
+        c = pso.track_frame(cf, x_gpu, 32, refine=True)
+        x_ref, _ = oracle.refine(ora_hand, obs, x_ref)
+        x_ref, _, _ = oracle.pso_evolve(ora_hand, obs, x_ref, 32, 6, lb, ub, sd)
+        cr = oracle.cal_cost(ora_hand, obs, x_ref)
+        np.testing.assert_allclose(x_gpu, x_ref, rtol=0, atol=1e-6)
+        assert abs(c - cr) <= 1e-8 * abs(cr)
+
+
+def test_edge_small_clouds(oracle, ora_hand, gpu_hand):
+    """N = 1 and the degenerate down-sample (N_full < 250 -> 250 copies of point 0)."""
+    import hpe
+    d = np.zeros((240, 320), np.float32)
+    d[120:125, 150:160] = 320.0  # 50 pixels at 32 cm
+    for ds in (True, False):
+        obs = oracle.preprocess(d, downsample=ds)
+        om = hpe.observedmodel(); om.downsample = ds; om.set_depth_mm(d)
+        cf = hpe.costfunc(gpu_hand, om)
+        th = np.vstack([oracle_np.X0, oracle_np.X0 + 3])
+        np.testing.assert_allclose(cf.cal_cost_batch(th), oracle.eval_costs(ora_hand, obs, th),
+                                   rtol=RTOL)
+    d1 = np.zeros((240, 320), np.float32); d1[100, 200] = 300.0
+    obs = oracle.preprocess(d1, downsample=False)
+    om = hpe.observedmodel(); om.set_depth_mm(d1)
+    cf = hpe.costfunc(gpu_hand, om)
+    np.testing.assert_allclose(cf.cal_cost_batch(oracle_np.X0[None]),
+                               oracle.eval_costs(ora_hand, obs, oracle_np.X0[None]), rtol=RTOL)
