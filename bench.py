@@ -1,0 +1,242 @@
+#!/usr/bin/env python3
+"""bench.py -- particle-evals/s + tracked FPS of the MI355X PSO hand tracker.
+
+Workload (BASELINE.json configs[1]/[2]): a step is ONE TRACKED FRAME of a synthetic
+240x320 depth sequence -- refine_init_pose, pso_evolve with 256 particles x 30
+generations (reference maxiter = 31), cal_cost(bestp), x0 <- bestp -- exactly the body
+of test_full (testmodel.cpp:124-138), on frames already preprocessed and resident in
+HBM.  N = 250 cloud points (the reference's downsample=true default).
+
+  value        = PSO particle evaluations per second over all ranks
+                 (P*(G+1) per frame per rank; refine and final evaluations are not counted)
+  tracked_fps  = frames per second (per rank; ranks track the same sequence)
+  multi-GPU    = one process per GPU, independent subswarms (seed 1000+rank) with one
+                 RCCL all-gather of {bestp, cost} per frame; weak scaling
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (N > 1 is launched by torch.distributed.run, one rank per GPU)
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "hand-pose-estimation_amd"))
+
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
+FP32_PEAK_TFLOPS = 157.3  # vector fp32 (spec); the search is fp32 VALU, no MFMA
+
+
+def algorithmic_bytes_per_eval(n: int) -> int:
+    # cloud xyz fp64 (24 B/pt) + 48 x (depth fp64 + DT fp32) gathers
+    # + PSO state: read x, v, pbest, pbest[informant]; write x, v, pbest (7 x 26 fp64)
+    # + pcost read/write (16 B)                                       
+    return 24 * n + 48 * 12 + 7 * 26 * 8 + 16
+
+
+def algorithmic_flops_per_eval(n: int) -> int:
+    # 8 flops per point-sphere pair + 11 per point (alignment)
+    # + ~960 (depth) + ~5500 (FK)
+    return 8 * 48 * n + 11 * n + 960 + 5500
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--particles", type=int, default=256)
+    ap.add_argument("--generations", type=int, default=30)
+    ap.add_argument("--full-cloud", action="store_true", help="no down-sampling (N ~ 9.3k)")
+    ap.add_argument("--no-refine", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--seed", type=int, default=0, help="trajectory seed")
+    return ap.parse_args()
+
+
+def cpu_baseline(args, sizes_hint):
+    """The oracle (C restatement, OpenMP over particles where the reference has
+    `omp parallel for`) tracking the same synthetic frames on the host: a bounded
+    sample of the same workload."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import numpy as np
+    import oracle_c
+    import oracle_np
+    import hpe
+    from hpe import synth
+    o = oracle_c.load(build=False)
+    d = json.loads((ROOT / "hand-pose-estimation_amd/hpe/hand_subject1.json").read_text())
+    geo, rad = np.array(d["hgeo_mm"]) / 10.0, np.array(d["rad_mm"]) / 10.0
+    h = o.hand(geo, rad)
+    nh = oracle_np.Hand(geo, rad)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
+    P, G = args.particles, args.generations
+    ub, lb, sd = hpe.reference_bounds()
+    poses = synth.trajectory(64, args.seed)
+    frames = [o.preprocess(oracle_np.render_depth_mm(nh, poses[f]),
+                           downsample=not args.full_cloud) for f in range(min(len(poses), 64))]
+    x = poses[0].copy()
+    done, t0 = 0, time.perf_counter()
+    while True:
+        obs = frames[done % len(frames)]
+        if not args.no_refine:
+            x, _ = o.refine(h, obs, x)
+        x, _, _ = o.pso_evolve(h, obs, x, P, G + 1, lb, ub, sd, seed=1000, nthreads=threads)
+        o.cal_cost(h, obs, x)
+        done += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds or done >= 4096:
+            break
+    return {"value": P * (G + 1) * done / el, "unit": "particle-evals/s", "cores": threads,
+            "kind": "port", "tracked_fps": done / el,
+            "sample": f"{done} tracked frames ({P}p x {G} gen, N={frames[0].n}, "
+                      f"refine={'off' if args.no_refine else 'on'}) of the same synthetic "
+                      f"sequence in {el:.1f} s, oracle/hpe_oracle.c with {threads} OpenMP threads"}
+
+
+def load_pmc(P, n_points):
+    """HBM traffic per k_pso_gen launch from the committed rocprofv3 --pmc summary."""
+    p = ROOT / "profiles" / "pmc_k_pso_gen.json"
+    if not p.exists():
+        return None
+    try:
+        d = json.loads(p.read_text())
+        if d.get("particles") == P and d.get("cloud_points") == n_points:
+            return d.get("bytes_per_launch")
+    except Exception:
+        return None
+    return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with "
+                         "torch.distributed.run")
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import hpe
+    from hpe import synth
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    P, G = args.particles, args.generations
+    hand = hpe.reference_hand(device=local)
+    ctx, lib = hand.ctx, hand.ctx.lib
+    n_frames = args.warmup + args.steps
+    poses, sizes = synth.load_sequence(ctx, n_frames, seed=args.seed,
+                                       downsample=not args.full_cloud)
+    ub, lb, sd = hpe.reference_bounds()
+    ctx.check(lib.hpe_set_pso_params(ctx.h, hpe._lib.ptr(ub, C.c_double),
+                                     hpe._lib.ptr(lb, C.c_double), hpe._lib.ptr(sd, C.c_double),
+                                     0.7298, 1.49618, 1.49618, G + 1, 1e-8, 1e-8))
+    ctx.check(lib.hpe_set_seed(ctx.h, C.c_uint64(1000 + rank)))
+    state = torch.zeros(27, dtype=torch.float64, device=f"cuda:{local}")
+    state[:26] = torch.from_numpy(poses[0])
+    torch.cuda.synchronize()
+    ext = torch.cuda.ExternalStream(lib.hpe_stream(ctx.h), device=f"cuda:{local}")
+    gathered = torch.zeros(world * 27, dtype=torch.float64, device=f"cuda:{local}")
+    refine = 0 if args.no_refine else 1
+
+    def step(f):
+        ctx.select_frame(f)
+        ctx.check(lib.hpe_track_frame_dev(ctx.h, P, refine, C.c_void_p(state.data_ptr())))
+        if world > 1:  # best-of-N exchange on the tracker's own stream (no host sync)
+            with torch.cuda.stream(ext):
+                dist.all_gather_into_tensor(gathered, state)
+                g = gathered.view(world, 27)
+                state.copy_(g[torch.argmin(g[:, 26])])
+
+    for f in range(args.warmup):
+        step(f)
+    ctx.check(lib.hpe_sync(ctx.h))
+    torch.cuda.synchronize()
+    ctx.check(lib.hpe_profile_enable(ctx.h, 1))
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for f in range(args.warmup, n_frames):
+        step(f)
+    ctx.check(lib.hpe_sync(ctx.h))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    nl = C.c_int32(0); tot = C.c_double(0); mn = C.c_double(0); mx = C.c_double(0)
+    ctx.check(lib.hpe_profile_read(ctx.h, C.byref(nl), C.byref(tot), C.byref(mn), C.byref(mx)))
+    ctx.check(lib.hpe_profile_enable(ctx.h, 0))
+    final = state.cpu().numpy()
+
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+    n_pts = sizes[args.warmup]
+    evals = P * (G + 1) * args.steps * world
+    avg_ms = tot.value / max(nl.value, 1)
+    bytes_launch = P * algorithmic_bytes_per_eval(n_pts)
+    flops_launch = P * algorithmic_flops_per_eval(n_pts)
+    achieved = bytes_launch / (avg_ms * 1e-3) / 1e9 if nl.value else None
+    line = {
+        "metric": "particle-evals/sec + tracked FPS, 320x240 depth, 256p x 30gen",
+        "value": evals / el,
+        "unit": "particle-evals/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32+f64",
+        "data": "synthetic: seeded 26-DOF trajectory rendered from the 48-sphere model "
+                "into 240x320 float32 mm depth (no MSRA Subject1 on the box)",
+        "config": {"workload": "tracked frame = refine_init_pose + pso_evolve + cal_cost(bestp)",
+                   "particles": P, "generations": G, "maxiter": G + 1,
+                   "cloud_points": n_pts, "refine": bool(refine),
+                   "parallelism": f"subswarms x{world}, all-gather best per frame"},
+        "tracked_fps": args.steps / el,
+        "final_cost": float(final[26]),
+        "roofline": {
+            "bound": "hbm", "kernel": "k_pso_gen",
+            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS if achieved else None,
+            "traffic": load_pmc(P, n_pts),
+            "avg_launch_us": avg_ms * 1e3, "launches": nl.value,
+            "min_launch_us": mn.value * 1e3, "max_launch_us": mx.value * 1e3,
+            "bytes_per_launch": bytes_launch,
+            "valu_tflops": flops_launch / (avg_ms * 1e-3) / 1e12 if nl.value else None,
+            "valu_frac": flops_launch / (avg_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS
+            if nl.value else None,
+            "note": "algorithmic bytes per launch = P*(24N + 2048); the fp32 search is "
+                    "VALU-bound, see valu_frac (DESIGN.md §5)"},
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args, sizes)
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

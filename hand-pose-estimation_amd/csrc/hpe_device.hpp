@@ -1,80 +1,130 @@
-// hpe_device.hpp -- device data layout and block-cooperative building blocks of the
-// MI355X PSO / costfunc / handmodel hot path (gfx950, wave64).
+// hpe_device.hpp -- device building blocks of the MI355X PSO / costfunc / handmodel
+// hot path (gfx950, wave64).
 //
-// One workgroup (HPE_NT = 512 threads = 8 waves) evaluates one particle:
-//   fk_block      26-DOF forward kinematics -> 48 sphere centres (fp64) in LDS
+//   fk_wave       26-DOF forward kinematics of one particle by ONE wave -> 48 sphere
+//                 centres (fp64 + fp32 copies) in that wave's LDS workspace
 //                 (handmodel.cpp:259-298, fingermodel.cpp:70-317, thumbmodel.cpp:76-318)
-//   match_align   N x 48 nearest-centre search (fp32, BFMatcher semantics) fused
-//                 with the fp64 alignment residual (costfunc.cpp:306-377)
-//   depth/collide 48 projections + depth/DT gathers, 144 collision pairs
-//                 (costfunc.cpp:227-304, 130-197)
-// The file is compiled with -ffp-contract=off: every product is rounded before the
-// add, as in the x86-64 reference build; the structured matrix products below skip
-// only terms that are exact zeros (x + a*0 == x) or exact unit factors (a*1 == a),
-// so they reproduce the reference's 4x4 k-ordered sums bit for bit.
+//   search_align  N x 48 nearest-centre search (fp32, BFMatcher semantics) fused with
+//                 the fp64 alignment residual, by NT threads      (costfunc.cpp:306-377)
+//   depth_term / collide_term                                  (costfunc.cpp:227-304, 130-197)
+//   eval_block    one particle per workgroup (PSO generations, batch evaluation)
+//   eval_wave     one particle per wave with frozen correspondences (refine)
+//
+// Compiled with -ffp-contract=off: every product is rounded before the add, as in the
+// x86-64 reference build.  The structured matrix products skip only terms that are
+// exact zeros (x + a*0 == x for finite a) or exact unit factors (a*1 == a), so they
+// reproduce the reference's k-ordered 4x4 sums bit for bit; only sin/cos (ocml vs
+// glibc, both < 1 ulp) can differ.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "hpe_layout.hpp"
 
-struct __align__(16) Smem {
-    float4 Sf[HPE_NS];        // fp32 centres for the search
-    double S[HPE_NS][3];      // fp64 centres, y/z negated
-    double AB[5][12];
-    double J[5][5][3];        // joints per digit (hand_joints source)
-    double th[32];
-    double sn[24], cs[24];
-    double red[HPE_NW][4];
-    double dscal[8];
-    int iscal[8];
+// Diagnostic phase stamps (libhpe_stamps.so only, -DHPE_STAMPS=1; the product build
+// compiles them out).  Thread 0 of block 0 accumulates shader-clock cycles per phase.
+#ifndef HPE_STAMPS
+#define HPE_STAMPS 0
+#endif
+__device__ unsigned long long hpe_stamps[64];
+struct StampClock {
+    unsigned long long t;
+    __device__ __forceinline__ void start() {
+        if (HPE_STAMPS && blockIdx.x == 0 && threadIdx.x == 0) t = __builtin_amdgcn_s_memtime();
+    }
+    __device__ __forceinline__ void lap(int k) {
+        if (HPE_STAMPS && blockIdx.x == 0 && threadIdx.x == 0) {
+            const unsigned long long n = __builtin_amdgcn_s_memtime();
+            hpe_stamps[k] += n - t;
+            hpe_stamps[32 + k] += 1;
+            t = n;
+        }
+    }
 };
+
+// Per-evaluating-wave LDS workspace.
+struct __align__(16) FkSm {
+    float4 Sf[HPE_NS];       // fp32 centres for the search
+    double S[HPE_NS][3];     // fp64 centres, y/z negated (handmodel.cpp:288)
+    double J[5][5][3];       // joints per digit (hand_joints source)
+    double th[32];           // the particle
+    double sn[24], cs[24];   // 3 global + 20 digit angles
+};
+
+// Block-level workspace (one particle per workgroup).
+struct __align__(16) Smem {
+    DevHand hand;  // hand constants staged from HBM (lane-indexed reads stay in LDS)
+    FkSm fk;
+    double red[16][4];
+    double dscal[8];
+    int iscal[16];
+};
+
+// Cloud + correspondences, either in LDS (staged) or in HBM.
+struct CloudView {
+    const double *cx, *cy, *cz;
+    int n;
+};
+
+// Copy the hand constants into LDS; caller synchronises before use.
+template <int NT>
+__device__ __forceinline__ void stage_hand(DevHand &dst, const DevHand *__restrict__ src) {
+    static_assert(sizeof(DevHand) % 8 == 0, "DevHand must be a multiple of 8 bytes");
+    for (int q = threadIdx.x; q < (int)(sizeof(DevHand) / 8); q += NT)
+        ((double *)&dst)[q] = ((const double *)src)[q];
+}
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 __device__ __forceinline__ double deg2rad(double a) {
     return a / 180.0 * 3.141592653589793115997963468544185161590576171875;  // fingermodel.cpp:203
 }
 
-// ---------------------------------------------------------------- FK
-// Step A: 23 lanes, one sincos each (3 global + 20 digit angles).
-// Step B: 60 lanes, one entry each of AB = A(a1)*B(a2) per digit (T12*T23 / T01*T12).
-// Step C: 15 lanes (digit, row): each carries ONE ROW of the left-multiplied chain
-//         cur = T00*Tgb*F*AB*C3*C4 -- row r of a left product depends only on row r
-//         of the left factor, so no exchange is needed -- and writes coordinate r of
-//         that digit's spheres.
-__device__ __forceinline__ void fk_block(Smem &sm, const DevHand *__restrict__ H) {
-    const int t = threadIdx.x;
-    if (t < 23) {
+// ---------------------------------------------------------------- FK (one wave)
+// Phase 1: 23 lanes, one sincos each (TWS, ANG, ROT and the 20 digit angles).
+// Phase 2: 15 lanes (digit d, row r).  Row r of a left-multiplied product depends only
+//          on row r of the left factor, so each lane carries ONE ROW of
+//          cur = T00*Tgb*F*(A*B)*C3*C4 with no exchange; the 9 entries of A*B it needs
+//          (T12*T23 / T01*T12) are independent of the chain and overlap with it.  The
+//          lane then writes coordinate r of its digit's spheres.
+__device__ __forceinline__ void fk_wave(FkSm &f, const DevHand *__restrict__ H) {
+    const int l = threadIdx.x & 63;
+    StampClock sc;
+    sc.start();
+    if (l < 23) {
         double a;
-        if (t == 0) a = deg2rad(sm.th[0] + 180);  // TWS, fingermodel.cpp:91
-        else if (t < 3) a = deg2rad(sm.th[t]);    // ANG, ROT
-        else a = deg2rad(sm.th[6 + (t - 3)]);     // digit angles, handmodel.cpp:141-146
+        if (l == 0) a = deg2rad(f.th[0] + 180);  // TWS, fingermodel.cpp:91
+        else if (l < 3) a = deg2rad(f.th[l]);    // ANG, ROT
+        else a = deg2rad(f.th[6 + (l - 3)]);     // digit angles, handmodel.cpp:141-146
         double s, c;
         sincos(a, &s, &c);
-        sm.sn[t] = s;
-        sm.cs[t] = c;
+        f.sn[l] = s;
+        f.cs[l] = c;
     }
-    __syncthreads();
-    if (t < 60) {
-        const int d = t / 12, e = t % 12, i = e >> 2, j = e & 3;
-        const double c1 = sm.cs[3 + 4 * d], s1 = sm.sn[3 + 4 * d];
-        const double c2 = sm.cs[4 + 4 * d], s2 = sm.sn[4 + 4 * d];
-        const double L1 = H->L[d][1], tc = H->twc[d], ts = H->tws[d];
-        double a0, a1, a2;  // row i of A = [[c1,0,-s1,0],[s1,0,c1,0],[0,-1,0,0]]
-        if (i == 0) { a0 = c1; a1 = 0; a2 = -s1; }
-        else if (i == 1) { a0 = s1; a1 = 0; a2 = c1; }
-        else { a0 = 0; a1 = -1; a2 = 0; }
-        double b0, b1, b2;  // column j of B (thumbmodel.cpp:150-153; fingers: tc=1, ts=0)
-        if (j == 0) { b0 = c2; b1 = s2; b2 = 0; }
-        else if (j == 1) { b0 = -s2 * tc; b1 = c2 * tc; b2 = ts; }
-        else if (j == 2) { b0 = s2 * ts; b1 = -c2 * ts; b2 = tc; }
-        else { b0 = L1 * c2; b1 = L1 * s2; b2 = 0; }
-        sm.AB[d][e] = (a0 * b0 + a1 * b1) + a2 * b2;  // + A(i,3)*B(3,j) = +0
-    }
-    __syncthreads();
-    if (t < 15) {
-        const int d = t / 3, r = t % 3;
-        const double cz = sm.cs[0], sz = sm.sn[0], cy = sm.cs[1], sy = sm.sn[1];
-        const double cxr = sm.cs[2], sxr = sm.sn[2];
+    wave_sync();
+    sc.lap(13);
+    if (l < 15) {
+        const int d = l / 3, r = l - 3 * (l / 3);
+        const double c1 = f.cs[3 + 4 * d], s1 = f.sn[3 + 4 * d];
+        const double c2 = f.cs[4 + 4 * d], s2 = f.sn[4 + 4 * d];
+        const double c3 = f.cs[5 + 4 * d], s3 = f.sn[5 + 4 * d];
+        const double c4 = f.cs[6 + 4 * d], s4 = f.sn[6 + 4 * d];
+        const double L1 = H->L[d][1], L2 = H->L[d][2], L3 = H->L[d][3];
+        const double tc = H->twc[d], ts = H->tws[d];
+        // Columns 0, 1, 3 of A*B with A = [[c1,0,-s1,0],[s1,0,c1,0],[0,-1,0,0]] and
+        // B = [[c2,-s2*tc,s2*ts,L1*c2],[s2,c2*tc,-c2*ts,L1*s2],[0,ts,tc,0]]
+        // (thumbmodel.cpp:144-153; fingers tc = 1, ts = 0, fingermodel.cpp:137-145).
+        // Each entry is the reference's k-ordered sum with its exact-zero terms dropped.
+        const double b01 = -s2 * tc, b11 = c2 * tc, L1c2 = L1 * c2, L1s2 = L1 * s2;
+        const double AB00 = c1 * c2, AB10 = s1 * c2, AB20 = -s2;
+        const double AB01 = c1 * b01 + (-s1) * ts, AB11 = s1 * b01 + c1 * ts, AB21 = -b11;
+        const double AB03 = c1 * L1c2, AB13 = s1 * L1c2, AB23 = -L1s2;
+        const double cz = f.cs[0], sz = f.sn[0], cy = f.cs[1], sy = f.sn[1];
+        const double cxr = f.cs[2], sxr = f.sn[2];
         double z0, z1, z2;  // row r of Rz
         if (r == 0) { z0 = cz; z1 = -sz; z2 = 0; }
         else if (r == 1) { z0 = sz; z1 = cz; z2 = 0; }
@@ -87,7 +137,7 @@ __device__ __forceinline__ void fk_block(Smem &sm, const DevHand *__restrict__ H
         const double g0 = q0;
         const double g1 = q1 * cxr + q2 * sxr;
         const double g2 = q1 * (-sxr) + q2 * cxr;
-        const double u = sm.th[3 + r];
+        const double u = f.th[3 + r];
         // cur1 = cur0 * F  (rotation about z + translation L0)
         const double h0 = g0 * H->Fc[d] + g1 * H->Fs[d];
         const double h1 = g0 * (-H->Fs[d]) + g1 * H->Fc[d];
@@ -96,76 +146,95 @@ __device__ __forceinline__ void fk_block(Smem &sm, const DevHand *__restrict__ H
         const double J1 = h3;
         const double J0 = (h0 * H->T10x[d] + h1 * H->T10y[d]) + h3;  // (cur*T10) at i == 1
         // cur2 = cur1 * AB
-        const double *AB = sm.AB[d];
-        const double k0 = (h0 * AB[0] + h1 * AB[4]) + h2 * AB[8];
-        const double k1 = (h0 * AB[1] + h1 * AB[5]) + h2 * AB[9];
-        const double k3 = ((h0 * AB[3] + h1 * AB[7]) + h2 * AB[11]) + h3;
+        const double k0 = (h0 * AB00 + h1 * AB10) + h2 * AB20;
+        const double k1 = (h0 * AB01 + h1 * AB11) + h2 * AB21;
+        const double k3 = ((h0 * AB03 + h1 * AB13) + h2 * AB23) + h3;
         const double J2 = k3;
-        // cur3 = cur2 * C3, C4 translation only
-        const double c3 = sm.cs[5 + 4 * d], s3 = sm.sn[5 + 4 * d];
-        const double c4 = sm.cs[6 + 4 * d], s4 = sm.sn[6 + 4 * d];
-        const double L2 = H->L[d][2], L3 = H->L[d][3];
+        // cur3 = cur2 * C3, then the translation of cur3 * C4
         const double m0 = k0 * c3 + k1 * s3;
         const double m1 = k0 * (-s3) + k1 * c3;
         const double m3 = (k0 * (L2 * c3) + k1 * (L2 * s3)) + k3;
         const double J3 = m3;
         const double J4 = (m0 * (L3 * c4) + m1 * (L3 * s4)) + m3;
-        const double J[5] = {J0, J1, J2, J3, J4};
+        f.J[d][0][r] = J0;
+        f.J[d][1][r] = J1;
+        f.J[d][2][r] = J2;
+        f.J[d][3][r] = J3;
+        f.J[d][4][r] = J4;
+    }
+    wave_sync();
+    // spheres (fingermodel.cpp:208-267, thumbmodel.cpp:227-274): 144 (sphere, coord)
+    // items over the wave, weights from the hand tables; cols(1,2) *= -1 (handmodel.cpp:288)
 #pragma unroll
-        for (int k = 0; k < 5; ++k) sm.J[d][k][r] = J[k];
-        // spheres (fingermodel.cpp:208-267, thumbmodel.cpp:227-274)
-        const double sg = (r == 0) ? 1.0 : -1.0;  // cols(1,2) *= -1 (handmodel.cpp:288)
-        int idx = (d == 0) ? 0 : 8 + 10 * (d - 1);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            if (i == 0 && d != 0) {
-                const double tt = 1. / 3;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const double v = (1. - tt * j) * J[0] + (tt * j) * J[1];
-                    sm.S[idx][r] = v * sg;
-                    ((float *)&sm.Sf[idx])[r] = (float)(v * sg);
-                    ++idx;
-                }
-            } else {
-#pragma unroll
-                for (int j = 1; j < 3; ++j) {
-                    const double v = (1. - 0.5 * j) * J[i] + (0.5 * j) * J[i + 1];
-                    sm.S[idx][r] = v * sg;
-                    ((float *)&sm.Sf[idx])[r] = (float)(v * sg);
-                    ++idx;
-                }
-            }
+    for (int q = 0; q < 3; ++q) {
+        const int it = l + 64 * q;
+        if (it < 3 * HPE_NS) {
+            const int s = it / 3, r = it - 3 * (it / 3), d = H->dg[s], a = H->ja[s];
+            const double v = H->wa[s] * f.J[d][a][r] + H->wb[s] * f.J[d][a + 1][r];
+            const double vs = (r == 0) ? v : v * -1;
+            f.S[s][r] = vs;
+            ((float *)&f.Sf[s])[r] = (float)vs;
         }
     }
-    __syncthreads();
+    wave_sync();
+    sc.lap(14);
 }
 
 // ---------------------------------------------------------------- reductions
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+// Wave-wide fp64 sum without LDS: DPP butterflies inside each 16-lane row, then the four
+// row sums are combined in a fixed order through v_readlane.  Deterministic; all lanes
+// receive the total.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double row_sum16(double v) {
+    v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+    v += dpp_f64<0x141>(v);  // row_half_mirror
+    v += dpp_f64<0x140>(v);  // row_mirror
     return v;
 }
+__device__ __forceinline__ double wave_sum(double v) {
+    v = row_sum16(v);
+    return ((readlane_f64(v, 0) + readlane_f64(v, 16)) + readlane_f64(v, 32)) +
+           readlane_f64(v, 48);
+}
+// three independent sums interleaved for ILP
+__device__ __forceinline__ void wave_sum3(double &a, double &b, double &c) {
+    a += dpp_f64<0xB1>(a); b += dpp_f64<0xB1>(b); c += dpp_f64<0xB1>(c);
+    a += dpp_f64<0x4E>(a); b += dpp_f64<0x4E>(b); c += dpp_f64<0x4E>(c);
+    a += dpp_f64<0x141>(a); b += dpp_f64<0x141>(b); c += dpp_f64<0x141>(c);
+    a += dpp_f64<0x140>(a); b += dpp_f64<0x140>(b); c += dpp_f64<0x140>(c);
+    a = ((readlane_f64(a, 0) + readlane_f64(a, 16)) + readlane_f64(a, 32)) + readlane_f64(a, 48);
+    b = ((readlane_f64(b, 0) + readlane_f64(b, 16)) + readlane_f64(b, 32)) + readlane_f64(b, 48);
+    c = ((readlane_f64(c, 0) + readlane_f64(c, 16)) + readlane_f64(c, 32)) + readlane_f64(c, 48);
+}
 
-// Sum three per-thread doubles over the block in a fixed order; result in every thread.
-__device__ __forceinline__ void block_sum3(Smem &sm, double &a, double &b, double &c) {
-    a = wave_sum(a);
-    b = wave_sum(b);
-    c = wave_sum(c);
+// Sum three per-thread doubles over NT threads in a fixed order; result in every thread.
+template <int NT>
+__device__ __forceinline__ void block_sum3(double (*red)[4], double &a, double &b, double &c) {
+    wave_sum3(a, b, c);
     const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
-        sm.red[w][0] = a;
-        sm.red[w][1] = b;
-        sm.red[w][2] = c;
+        red[w][0] = a;
+        red[w][1] = b;
+        red[w][2] = c;
     }
     __syncthreads();
     double ra = 0, rb = 0, rc = 0;
 #pragma unroll
-    for (int k = 0; k < HPE_NW; ++k) {
-        ra += sm.red[k][0];
-        rb += sm.red[k][1];
-        rc += sm.red[k][2];
+    for (int k = 0; k < NT / 64; ++k) {
+        ra += red[k][0];
+        rb += red[k][1];
+        rc += red[k][2];
     }
     a = ra;
     b = rb;
@@ -175,9 +244,9 @@ __device__ __forceinline__ void block_sum3(Smem &sm, double &a, double &b, doubl
 
 // ---------------------------------------------------------------- cost terms
 // depth_penalty term of sphere i (costfunc.cpp:249-300); S is un-negated on the fly.
-__device__ __forceinline__ double depth_term(const Smem &sm, int i, const DevObs &o,
+__device__ __forceinline__ double depth_term(const FkSm &f, int i, const DevObs &o,
                                              const DevHand *__restrict__ H) {
-    const double x = sm.S[i][0], y = sm.S[i][1] * -1, z = sm.S[i][2] * -1;
+    const double x = f.S[i][0], y = f.S[i][1] * -1, z = f.S[i][2] * -1;
     const double pu = (o.K[0] * x + o.K[1] * y) + o.K[2] * z;
     const double pv = (o.K[3] * x + o.K[4] * y) + o.K[5] * z;
     const double pw = (o.K[6] * x + o.K[7] * y) + o.K[8] * z;
@@ -188,7 +257,7 @@ __device__ __forceinline__ double depth_term(const Smem &sm, int i, const DevObs
         const double djc = o.depth[pix];
         if (djc != 0.0) {
             const double tt = djc - z;
-            const double diff = (0.0 < tt) ? tt : 0.0;
+            const double diff = (0.0 < tt) ? tt : 0.0;  // std::max(0.0, tt)
             return diff * diff;
         }
         const double dd = (double)o.dt[pix] * o.scale + r;
@@ -199,20 +268,20 @@ __device__ __forceinline__ double depth_term(const Smem &sm, int i, const DevObs
 }
 
 // one of the 144 self-collision pairs (costfunc.cpp:150-193)
-__device__ __forceinline__ double collide_term(const Smem &sm, int t,
+__device__ __forceinline__ double collide_term(const FkSm &f, int t,
                                                const DevHand *__restrict__ H) {
     const int p = t / 36, k = t % 36;
     const int a = 2 + 10 * p + k / 6, b = 2 + 10 * (p + 1) + k % 6;
-    const double dx = sm.S[b][0] - sm.S[a][0], dy = sm.S[b][1] - sm.S[a][1],
-                 dz = sm.S[b][2] - sm.S[a][2];
+    const double dx = f.S[b][0] - f.S[a][0], dy = f.S[b][1] - f.S[a][1],
+                 dz = f.S[b][2] - f.S[a][2];
     const double v = (H->radii[b] + H->radii[a]) - sqrt((dx * dx + dy * dy) + dz * dz);
     return v > 0 ? v * v : 0.0;
 }
 
 // Largest float whose correctly rounded sqrt equals sqrtf(m): BFMatcher compares
-// sqrtf(d2) (OpenCV batchDistL2_32f) with first-index ties, so the match is the
-// first j with d2[j] <= hi_sqrt_class(min_j d2[j]).  sqrt double->float is
-// innocuous double rounding (53 >= 2*24+2), mid^2 is exact in double.
+// sqrtf(d2) (OpenCV batchDistL2_32f) with first-index ties, so the match is the first
+// j with d2[j] <= hi_sqrt_class(min_j d2[j]).  double->float rounding of a double sqrt
+// is innocuous double rounding (53 >= 2*24+2); mid^2 is exact in double.
 __device__ __forceinline__ float hi_sqrt_class(float m) {
     const float s = (float)sqrt((double)m);
     const float sn = __uint_as_float(__float_as_uint(s) + 1u);
@@ -223,18 +292,41 @@ __device__ __forceinline__ float hi_sqrt_class(float m) {
     return h;
 }
 
-// Fused correspondence search + alignment residual.  Two lanes (t, t^1) share a point,
-// 24 spheres each; returns this thread's partial sum of (|p - S[m]| - r[m])^2.
-template <bool STORE_MATCH>
-__device__ __forceinline__ double match_align(const Smem &sm, const DevObs &o,
-                                              const DevHand *__restrict__ H,
-                                              int32_t *__restrict__ match) {
+// key = j if (bits(d2) <= hb) else j + 64, as three plain VALU ops (the compiler would
+// otherwise rebuild it as v_cmp + v_cndmask through VCC, one s_nop hazard each).
+template <int J>
+__device__ __forceinline__ int sqrt_class_key(int hb, float d2) {
+    int k;
+    asm("v_sub_u32 %0, %1, %2\n\tv_lshrrev_b32 %0, 31, %0\n\tv_lshl_or_b32 %0, %0, 6, %3"
+        : "=&v"(k)
+        : "v"(hb), "v"(__float_as_int(d2)), "i"(J));
+    return k;
+}
+
+// Fused correspondence search + alignment residual over NT threads.  Two lanes
+// (t, t^1) share a point, 24 spheres each; returns this thread's partial sum of
+// (|p - S[m]| - r[m])^2 and optionally stores m.
+struct Pt {
+    double x, y, z;
+};
+__device__ __forceinline__ Pt load_pt(const CloudView &cv, int it) {
+    const int p = it >> 1;
+    if (it < 2 * cv.n) return Pt{cv.cx[p], cv.cy[p], cv.cz[p]};
+    return Pt{0, 0, 0};
+}
+// pre: the point of item threadIdx.x, loaded early by the caller (load_pt) so its
+// latency hides under FK.
+template <int NT, bool STORE_MATCH>
+__device__ __forceinline__ double search_align(const FkSm &f, const CloudView &cv,
+                                               const DevHand *__restrict__ H,
+                                               int32_t *__restrict__ match, Pt pre) {
     double acc = 0.0;
     const int h = threadIdx.x & 1;
-    const float4 *Sf = sm.Sf + 24 * h;
-    for (int it = threadIdx.x; it < 2 * o.n; it += HPE_NT) {
+    const float4 *Sf = f.Sf + 24 * h;
+    for (int it = threadIdx.x; it < 2 * cv.n; it += NT) {
         const int p = it >> 1;
-        const double X = o.cx[p], Y = o.cy[p], Z = o.cz[p];
+        const Pt q = (it == (int)threadIdx.x) ? pre : load_pt(cv, it);
+        const double X = q.x, Y = q.y, Z = q.z;
         const float qx = (float)X, qy = (float)Y, qz = (float)Z;
         float d2[24];
         float m = __builtin_inff();
@@ -245,16 +337,28 @@ __device__ __forceinline__ double match_align(const Smem &sm, const DevObs &o,
             d2[j] = (t0 * t0 + t1 * t1) + t2 * t2;
             m = fminf(m, d2[j]);
         }
-        m = fminf(m, __shfl_xor(m, 1));
+        m = fminf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0xB1, 0xf, 0xf,
+                                                               false)));  // partner lane t^1
         const float hi = hi_sqrt_class(m);
-        int idx = 1 << 20;
+        // first j with d2[j] <= hi, branch-free: key_j = j, or j + 64 when d2[j] > hi
+        // (non-negative floats order like their bit patterns), then an integer min tree
+        const int hb = __float_as_int(hi);
+        int key[24];
+#define HPE_KEY(J) key[J] = sqrt_class_key<J>(hb, d2[J]);
+        HPE_KEY(0) HPE_KEY(1) HPE_KEY(2) HPE_KEY(3) HPE_KEY(4) HPE_KEY(5) HPE_KEY(6) HPE_KEY(7)
+        HPE_KEY(8) HPE_KEY(9) HPE_KEY(10) HPE_KEY(11) HPE_KEY(12) HPE_KEY(13) HPE_KEY(14)
+        HPE_KEY(15) HPE_KEY(16) HPE_KEY(17) HPE_KEY(18) HPE_KEY(19) HPE_KEY(20) HPE_KEY(21)
+        HPE_KEY(22) HPE_KEY(23)
+#undef HPE_KEY
 #pragma unroll
-        for (int j = 23; j >= 0; --j) idx = (d2[j] <= hi) ? j : idx;
-        idx += 24 * h;
-        idx = min(idx, __shfl_xor(idx, 1));
+        for (int j = 0; j < 24; j += 3) key[j] = min(min(key[j], key[j + 1]), key[j + 2]);
+        int idx = min(min(min(key[0], key[3]), min(key[6], key[9])),
+                      min(min(key[12], key[15]), min(key[18], key[21])));
+        idx = (idx >= 64) ? (1 << 20) : idx + 24 * h;
+        idx = min(idx, __builtin_amdgcn_mov_dpp(idx, 0xB1, 0xf, 0xf, false));
         if (h == 0) {
             if (idx >= HPE_NS) idx = 0;  // all-NaN point: reference is undefined (trainIdx -1)
-            const double dx = X - sm.S[idx][0], dy = Y - sm.S[idx][1], dz = Z - sm.S[idx][2];
+            const double dx = X - f.S[idx][0], dy = Y - f.S[idx][1], dz = Z - f.S[idx][2];
             const double e = sqrt((dx * dx + dy * dy) + dz * dz) - H->radii[idx];
             acc += e * e;
             if (STORE_MATCH) match[p] = idx;
@@ -263,40 +367,69 @@ __device__ __forceinline__ double match_align(const Smem &sm, const DevObs &o,
     return acc;
 }
 
-// Alignment with frozen correspondences (cal_cost2(..., compute_corr=false)).
-__device__ __forceinline__ double align_frozen(const Smem &sm, const DevObs &o,
+// Alignment with frozen correspondences (cal_cost2(..., compute_corr=false)) over
+// `stride` lanes starting at `lane0`; four points in flight per lane.
+__device__ __forceinline__ double align_one(const FkSm &f, const CloudView &cv,
+                                            const DevHand *__restrict__ H,
+                                            const int32_t *__restrict__ match, int p) {
+    const int idx = match[p];
+    const double dx = cv.cx[p] - f.S[idx][0], dy = cv.cy[p] - f.S[idx][1],
+                 dz = cv.cz[p] - f.S[idx][2];
+    const double e = sqrt((dx * dx + dy * dy) + dz * dz) - H->radii[idx];
+    return e * e;
+}
+__device__ __forceinline__ double align_frozen(const FkSm &f, const CloudView &cv,
                                                const DevHand *__restrict__ H,
-                                               const int32_t *__restrict__ match) {
-    double acc = 0.0;
-    for (int p = threadIdx.x; p < o.n; p += HPE_NT) {
-        const int idx = match[p];
-        const double dx = o.cx[p] - sm.S[idx][0], dy = o.cy[p] - sm.S[idx][1],
-                     dz = o.cz[p] - sm.S[idx][2];
-        const double e = sqrt((dx * dx + dy * dy) + dz * dz) - H->radii[idx];
-        acc += e * e;
+                                               const int32_t *__restrict__ match, int lane0,
+                                               int stride) {
+    // fixed trip count of 4 points per lane per chunk, predicated (no divergent tail)
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    for (int base = 0; base < cv.n; base += 4 * stride) {
+        const int p0 = base + lane0, p1 = p0 + stride, p2 = p1 + stride, p3 = p2 + stride;
+        const int n1 = cv.n - 1;
+        const double e0 = align_one(f, cv, H, match, min(p0, n1));
+        const double e1 = align_one(f, cv, H, match, min(p1, n1));
+        const double e2 = align_one(f, cv, H, match, min(p2, n1));
+        const double e3 = align_one(f, cv, H, match, min(p3, n1));
+        a0 += (p0 < cv.n) ? e0 : 0.0;
+        a1 += (p1 < cv.n) ? e1 : 0.0;
+        a2 += (p2 < cv.n) ? e2 : 0.0;
+        a3 += (p3 < cv.n) ? e3 : 0.0;
     }
-    return acc;
+    return (a0 + a1) + (a2 + a3);
 }
 
 enum EvalMode { EV_COST = 0, EV_COST2_CORR = 1, EV_COST2_FROZEN = 2, EV_COST_STORE = 3 };
 
-// Whole-block evaluation of the particle whose theta is in sm.th.  Every thread
-// returns the total; terms (align, depth, collision) optionally via sm.dscal[0..2].
-template <int MODE>
-__device__ __forceinline__ double eval_block(Smem &sm, const DevObs &o,
+__device__ __forceinline__ CloudView obs_cloud(const DevObs &o) {
+    return CloudView{o.cx, o.cy, o.cz, o.n};
+}
+
+// Whole-block evaluation of the particle in sm.fk.th (wave 0 does FK, NT threads the
+// search).  Every thread returns the total; terms (align, depth, collision) go to
+// sm.dscal[0..2].
+template <int MODE, int NT>
+__device__ __forceinline__ double eval_block(Smem &sm, const DevObs &o, const CloudView &cv,
                                              const DevHand *__restrict__ H,
-                                             int32_t *__restrict__ match) {
-    fk_block(sm, H);
+                                             int32_t *__restrict__ match, Pt pre) {
+    StampClock sc;
+    sc.start();
+    if (threadIdx.x < 64) fk_wave(sm.fk, H);
+    __syncthreads();
+    sc.lap(10);
     const int t = threadIdx.x;
     // issue the depth gathers first: their latency hides under the search
-    double dep = (t < HPE_NS) ? depth_term(sm, t, o, H) : 0.0;
+    double dep = (t < HPE_NS) ? depth_term(sm.fk, t, o, H) : 0.0;
     double al;
-    if (MODE == EV_COST2_FROZEN) al = align_frozen(sm, o, H, match);
-    else if (MODE == EV_COST2_CORR || MODE == EV_COST_STORE) al = match_align<true>(sm, o, H, match);
-    else al = match_align<false>(sm, o, H, nullptr);
+    if (MODE == EV_COST2_FROZEN) al = align_frozen(sm.fk, cv, H, match, t, NT);
+    else if (MODE == EV_COST2_CORR || MODE == EV_COST_STORE)
+        al = search_align<NT, true>(sm.fk, cv, H, match, pre);
+    else al = search_align<NT, false>(sm.fk, cv, H, nullptr, pre);
     const bool coll = (MODE == EV_COST2_CORR || MODE == EV_COST2_FROZEN);
-    double co = (coll && t < 144) ? collide_term(sm, t, H) : 0.0;
-    block_sum3(sm, al, dep, co);
+    double co = (coll && t < 144) ? collide_term(sm.fk, t, H) : 0.0;
+    sc.lap(11);
+    block_sum3<NT>(sm.red, al, dep, co);
+    sc.lap(12);
     const double align = al * o.lambda;
     if (t == 0) {
         sm.dscal[0] = align;
@@ -305,6 +438,29 @@ __device__ __forceinline__ double eval_block(Smem &sm, const DevObs &o,
     }
     if (!coll) return align + dep;
     return (align + dep) + co;
+}
+
+// One wave evaluates cal_cost2(f.th, match, false): FK, frozen alignment over the
+// whole cloud, depth, collision; wave-local synchronisation only.  All lanes return
+// the total.
+__device__ __forceinline__ double eval_wave_frozen(FkSm &f, const DevObs &o,
+                                                   const CloudView &cv,
+                                                   const DevHand *__restrict__ H,
+                                                   const int32_t *__restrict__ match) {
+    fk_wave(f, H);
+    StampClock sc;
+    sc.start();
+    const int l = threadIdx.x & 63;
+    double dep = (l < HPE_NS) ? depth_term(f, l, o, H) : 0.0;
+    sc.lap(15);
+    double al = align_frozen(f, cv, H, match, l, 64);
+    sc.lap(16);
+    double co = collide_term(f, l, H) + collide_term(f, l + 64, H) +
+                ((l < 16) ? collide_term(f, l + 128, H) : 0.0);
+    sc.lap(17);
+    wave_sum3(al, dep, co);
+    sc.lap(18);
+    return (al * o.lambda + dep) + co;
 }
 
 // ---------------------------------------------------------------- Philox4x32-10

@@ -42,6 +42,23 @@ void build_dev_hand(const hpe_hand_params &p, DevHand &h) {
         for (int k = 0; k < 4; ++k) h.L[d][k] = p.geo_cm[4 * d + k];
     }
     for (int i = 0; i < HPE_NS; ++i) h.radii[i] = p.radii_cm[i];
+    // sphere placement (fingermodel.cpp:223-265, thumbmodel.cpp:242-272):
+    // (1. - t*j) * joint1 + (t*j) * joint2, weights computed exactly as there
+    int s = 0;
+    for (int d = 0; d < 5; ++d) {
+        const int ns[4] = {d == 0 ? 2 : 4, 2, 2, 2};
+        for (int seg = 0; seg < 4; ++seg) {
+            const bool first = (seg == 0 && d != 0);
+            const double t = first ? 1. / (ns[0] - 1) : 1. / ns[seg];
+            const int j0 = first ? 0 : 1, j1 = first ? ns[0] : ns[seg] + 1;
+            for (int j = j0; j < j1; ++j, ++s) {
+                h.wa[s] = 1. - t * j;
+                h.wb[s] = t * j;
+                h.dg[s] = d;
+                h.ja[s] = seg;
+            }
+        }
+    }
 }
 
 // ---------------------------------------------------------------- preprocessing
@@ -176,29 +193,25 @@ void make_normals(uint64_t seed, int P, double *out) {
 }
 
 // Topology of generation t (PSO.cpp:790-803): each particle s links to
-// r = floor(u*(P-1) + 0.5) for 3 draws; receiver i's informants are {i} U {s -> i},
-// stored as an ascending-source CSR per generation.
-void make_links(uint64_t seed, int P, int G, std::vector<int> &off, std::vector<int> &src) {
-    off.assign((size_t)(G + 1) * (P + 1), 0);
-    src.assign((size_t)(G + 1) * 3 * P, 0);
-    std::vector<int> r(3 * (size_t)P), fill(P);
+// r = floor(u*(P-1) + 0.5) for 3 draws; receiver r's informants are {r} U {s -> r}.
+// outl[t][s][k] = (r, slot of s in r's ascending source list); K = max in-degree.
+int make_links(uint64_t seed, int P, int G, std::vector<int> &outl) {
+    outl.assign((size_t)(G + 1) * P * 6, -1);
+    std::vector<int> fill(P);
+    int K = 1;
     for (int t = 1; t <= G; ++t) {
-        int *o = &off[(size_t)t * (P + 1)];
-        int *s = &src[(size_t)t * 3 * P];
-        for (int q = 0; q < P; ++q)
-            for (int k = 0; k < 3; ++k) {
-                const double u = host_u01(seed, ST_LINK, t, q, k);
-                r[3 * q + k] = (int)std::floor(u * (P - 1) + 0.5);
-                o[r[3 * q + k] + 1]++;
-            }
-        for (int i = 0; i < P; ++i) o[i + 1] += o[i];
         std::fill(fill.begin(), fill.end(), 0);
-        for (int q = 0; q < P; ++q)
+        for (int s = 0; s < P; ++s)  // ascending s: slots follow the reference's find() order
             for (int k = 0; k < 3; ++k) {
-                const int dst = r[3 * q + k];
-                s[o[dst] + fill[dst]++] = q;
+                const double u = host_u01(seed, ST_LINK, t, s, k);
+                const int r = (int)std::floor(u * (P - 1) + 0.5);
+                int *o = &outl[(((size_t)t * P + s) * 3 + k) * 2];
+                o[0] = r;
+                o[1] = fill[r]++;
+                K = std::max(K, fill[r]);
             }
     }
+    return K;
 }
 
 }  // namespace hpe

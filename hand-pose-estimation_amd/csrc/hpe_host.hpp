@@ -17,5 +17,5 @@ int preprocess_depth(const float *depth_mm, int to_cm, int downsample, double fo
                      double *scale_out, double *dtmax_out, double K[9]);
 double host_u01(uint64_t seed, uint32_t stream, uint32_t gen, uint32_t idx, uint32_t k);
 void make_normals(uint64_t seed, int P, double *out);
-void make_links(uint64_t seed, int P, int G, std::vector<int> &off, std::vector<int> &src);
+int make_links(uint64_t seed, int P, int G, std::vector<int> &outl);
 }  // namespace hpe

@@ -13,25 +13,29 @@
 // One workgroup of HPE_NT threads per particle; see hpe_device.hpp for the block-level
 // pieces and DESIGN.md for layout, rooflines and the parity argument.
 #include "hpe_device.hpp"
+#include "../../include/hpe.h"
 
 // ------------------------------------------------------------------ batch kernels
 __global__ __launch_bounds__(HPE_NT) void k_build(const double *__restrict__ theta, int P,
-                                                  const DevHand *__restrict__ H,
+                                                  const DevHand *__restrict__ Hg,
                                                   double *__restrict__ S_out,
                                                   double *__restrict__ J_out) {
     __shared__ Smem sm;
     const int i = blockIdx.x, t = threadIdx.x;
-    if (t < HPE_DOF) sm.th[t] = theta[(size_t)i * HPE_DOF + t];
+    stage_hand<HPE_NT>(sm.hand, Hg);
+    const DevHand *__restrict__ H = &sm.hand;
+    if (t < HPE_DOF) sm.fk.th[t] = theta[(size_t)i * HPE_DOF + t];
     __syncthreads();
-    fk_block(sm, H);
-    if (t < 3 * HPE_NS) S_out[(size_t)i * 3 * HPE_NS + t] = (&sm.S[0][0])[t];
+    if (t < 64) fk_wave(sm.fk, H);
+    __syncthreads();
+    if (t < 3 * HPE_NS) S_out[(size_t)i * 3 * HPE_NS + t] = (&sm.fk.S[0][0])[t];
     if (J_out && t < 63) {  // hand_joints rows: wrist, index..little joints 1-4, thumb 1-4
         double v;
-        if (t < 3) v = sm.th[3 + t];
+        if (t < 3) v = sm.fk.th[3 + t];
         else {
             const int row = t / 3, c = t % 3, k = (row - 1) / 4, jr = 1 + (row - 1) % 4;
             const int d = (k < 4) ? k + 1 : 0;
-            v = sm.J[d][jr][c];
+            v = sm.fk.J[d][jr][c];
         }
         J_out[(size_t)i * 63 + t] = v;
     }
@@ -39,16 +43,20 @@ __global__ __launch_bounds__(HPE_NT) void k_build(const double *__restrict__ the
 
 template <int MODE>
 __global__ __launch_bounds__(HPE_NT) void k_eval(const double *__restrict__ theta, int P,
-                                                 DevObs o, const DevHand *__restrict__ H,
+                                                 DevObs o, const DevHand *__restrict__ Hg,
                                                  double *__restrict__ cost,
                                                  int32_t *__restrict__ match,
                                                  double *__restrict__ terms) {
     __shared__ Smem sm;
     const int i = blockIdx.x, t = threadIdx.x;
-    if (t < HPE_DOF) sm.th[t] = theta[(size_t)i * HPE_DOF + t];
+    stage_hand<HPE_NT>(sm.hand, Hg);
+    const DevHand *__restrict__ H = &sm.hand;
+    if (t < HPE_DOF) sm.fk.th[t] = theta[(size_t)i * HPE_DOF + t];
+    const CloudView cv = obs_cloud(o);
+    const Pt pre = load_pt(cv, t);
     __syncthreads();
     int32_t *m = match ? match + (size_t)i * o.n : nullptr;
-    const double c = eval_block<MODE>(sm, o, H, m);
+    const double c = eval_block<MODE, HPE_NT>(sm, o, cv, H, m, pre);
     if (t == 0) {
         cost[i] = c;
         if (terms) {
@@ -95,108 +103,161 @@ __device__ VI block_argmin(Smem &sm, VI mine) {
     return best;
 }
 
-// End-of-generation update (PSO.cpp:864-879) for the generation whose pbest costs are
-// pc (g_prev >= 1), or the initial gbest (PSO.cpp:755-760) when g_prev == 0.
-// Returns the new Sig; *improved / *fid say whether gbest_pos <- x[fid].
-__device__ Sig gbest_update(Smem &sm, const DevSwarm &sw, const double *__restrict__ pc,
-                            double *__restrict__ pcs_lds, int g_prev, Sig prev,
-                            bool *improved, int *fid) {
-    VI mine = {__builtin_inf(), 0};
-    for (int k = threadIdx.x; k < sw.P; k += HPE_NT) {
-        const double v = pc[k];
-        if (pcs_lds) pcs_lds[k] = v;
-        const double vv = nan_inf(v);
-        if (vv < mine.v) {
-            mine.v = vv;
-            mine.i = k;
-        }
-    }
-    const VI b = block_argmin(sm, mine);
-    Sig s;
-    if (g_prev == 0) {
-        *improved = b.v < 1e100;
-        s.gcost = *improved ? b.v : 1e100;
-        s.count = 100;  // PSO.cpp:768
-        s.topo = -1;
-    } else {
-        *improved = b.v < prev.gcost;
-        s.gcost = *improved ? b.v : prev.gcost;
-        s.count = *improved ? 0 : prev.count + 1;
-        s.topo = prev.topo;
-    }
-    *fid = b.i;
-    return s;
+#define IB_KMAX 24  // max informant in-degree handled (host checks K <= IB_KMAX)
+
+__device__ __forceinline__ double bits_to_f64(unsigned long long b) { return __longlong_as_double((long long)b); }
+__device__ __forceinline__ unsigned long long f64_to_bits(double v) {
+    return (unsigned long long)__double_as_longlong(v);
+}
+__device__ __forceinline__ size_t ib_index(const DevSwarm &sw, int par, int var, int r, int slot) {
+    return ((((size_t)par * 2 + var) * sw.P + r) * sw.K + slot) * IB_FIELDS;
+}
+
+// Push {tag = (g, s), pbest cost, pbest row} of particle s after generation g into the
+// inboxes of its receivers under the topology of generation g+1 (var 1) and under the
+// kept topology topo_g (var 0).  168 lanes: 6 destinations x 28 fields.
+__device__ __forceinline__ void push_inbox(const DevSwarm &sw, int g, int s, int topo_g,
+                                           double pc, const double *row) {
+    const int t = threadIdx.x;
+    if (g >= sw.G || t >= 6 * IB_FIELDS) return;
+    const int dst = t / IB_FIELDS, fld = t - IB_FIELDS * dst, var = dst < 3 ? 1 : 0;
+    const int tt = var ? g + 1 : topo_g;
+    if (tt < 1) return;
+    const int *o = sw.outl + (((size_t)tt * sw.P + s) * 3 + (dst % 3)) * 2;
+    const int r = o[0], slot = o[1];
+    // tag = (generation, topology, sender): a slot is only valid for the exact
+    // (g, topology) the reader expects, whatever an earlier call left behind.
+    const double val = (fld == 0) ? __longlong_as_double(((long long)g << 48) | ((long long)tt << 32) | s)
+                       : (fld == 1) ? pc : row[fld - 2];
+    sw.inbox[ib_index(sw, g & 1, var, r, slot) + fld] = val;
 }
 
 __global__ __launch_bounds__(HPE_NT) void k_pso_init(DevSwarm sw, const double *__restrict__ x0,
-                                                     DevObs o, const DevHand *__restrict__ H) {
+                                                     DevObs o, const DevHand *__restrict__ Hg) {
     __shared__ Smem sm;
     const int i = blockIdx.x, t = threadIdx.x;
+    stage_hand<HPE_NT>(sm.hand, Hg);
+    const DevHand *__restrict__ H = &sm.hand;
     const double *sd = sw.bounds + 2 * HPE_DOF;
     if (t < HPE_DOF) {  // particles = x0 + randn % std (PSO.cpp:67-72)
         const size_t e = (size_t)i * HPE_DOF + t;
         const double x = x0[t] + sw.normals[e] * sd[t];
-        sm.th[t] = x;
-        sw.x[0][e] = x;
-        sw.pb[0][e] = x;
+        sm.fk.th[t] = x;
+        sw.xh[e] = x;
+        sw.pb[e] = x;
         sw.v[e] = 0.0;
     }
+    const CloudView cv = obs_cloud(o);
+    const Pt pre = load_pt(cv, t);
     __syncthreads();
-    const double c = eval_block<EV_COST>(sm, o, H, nullptr);
-    if (t == 0) sw.pc[0][i] = c;
+    const double c = eval_block<EV_COST, HPE_NT>(sm, o, cv, H, nullptr, pre);
+    if (t == 0) {  // PSO.cpp:748-763; pbest costs are >= 0, so their bits order like values
+        sw.pch[i] = c;
+        atomicMin(&sw.gmin[0], f64_to_bits(c));
+    }
+    push_inbox(sw, 0, i, -1, c, sm.fk.th);
 }
 
+// One fused generation g >= 1 (PSO.cpp:781-879).  Round 1 loads everything: own state,
+// sig[g-1] / gmin[g-1] (previous generation's gbest bookkeeping) and the two inboxes.
 __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, DevObs o,
-                                                    const DevHand *__restrict__ H, int g,
+                                                    const DevHand *__restrict__ Hg, int g,
                                                     double W1, double C1, double C2) {
-    extern __shared__ double pcs[];  // pbest costs of generation g-1, P doubles
     __shared__ Smem sm;
-    const int i = blockIdx.x, t = threadIdx.x;
-    const int cur = g & 1, prv = cur ^ 1;
-    const double *__restrict__ pcp = sw.pc[prv];
-    // 1. gbest / count of the previous generation, topology of this one (PSO.cpp:790)
-    const Sig prev = (g >= 2) ? sw.sig[prv] : Sig{1e100, 100, -1};
-    bool improved;
-    int fid;
-    Sig s = gbest_update(sm, sw, pcp, pcs, g - 1, prev, &improved, &fid);
-    if (s.count > 0) s.topo = g;
-    if (i == 0) {
-        if (improved && t < HPE_DOF) sw.gpos[t] = sw.x[prv][(size_t)fid * HPE_DOF + t];
-        if (t == 0) {
-            sw.sig[cur] = s;
-            if (g >= 2 && sw.trace_g) {
-                sw.trace_g[g - 2] = s.gcost;
-                sw.trace_count[g - 2] = s.count;
-                sw.trace_topo[g - 2] = prev.topo;
-            }
+    __shared__ double ib[2][IB_KMAX][IB_FIELDS];
+    const int i = blockIdx.x, t = threadIdx.x, P = sw.P, K = sw.K;
+    stage_hand<HPE_NT>(sm.hand, Hg);
+    const DevHand *__restrict__ H = &sm.hand;
+    StampClock sc;
+    sc.start();
+    // ---- round 1: every load of this generation, all independent
+    const CloudView cv = obs_cloud(o);
+    const Pt pre = load_pt(cv, t);  // this thread's first cloud point, used after FK
+    double xo = 0, vo = 0, pbi = 0, rp = 0, rg = 0;
+    const size_t e = (size_t)i * HPE_DOF + t;
+    if (t < HPE_DOF) {
+        xo = sw.xh[(size_t)(g - 1) * P * HPE_DOF + e];
+        vo = sw.v[e];
+        pbi = sw.pb[e];
+        rp = philox_u01(sw.seed, ST_RP, g, i, t);
+        rg = philox_u01(sw.seed, ST_RG, g, i, t);
+    }
+    {
+        const double *src = sw.inbox + ib_index(sw, (g - 1) & 1, 0, i, 0);
+        const size_t var_stride = (size_t)P * K * IB_FIELDS;
+        for (int q = t; q < 2 * K * IB_FIELDS; q += HPE_NT) {
+            const int var = q / (K * IB_FIELDS), rem = q - var * K * IB_FIELDS;
+            (&ib[var][0][0])[rem] = src[var * var_stride + rem];
         }
     }
-    // 2. informant: first argmin of pbest cost over {i} U incoming links (PSO.cpp:810-812)
+    if (t == 64) sm.dscal[4] = sw.pch[(size_t)(g - 1) * P + i];  // own pbest cost
     if (t == 0) {
-        const int *off = sw.in_off + (size_t)s.topo * (sw.P + 1);
-        const int *src = sw.in_src + (size_t)s.topo * 3 * sw.P;
-        VI best = {nan_inf(pcs[i]), i};
-        for (int e = off[i]; e < off[i + 1]; ++e) {
-            const int q = src[e];
-            const VI c = {nan_inf(pcs[q]), q};
-            if (vi_less(c, best)) best = c;
+        // end-of-generation update of g-1 (PSO.cpp:864-877) / initial gbest (:755-760)
+        const double fmin = bits_to_f64(sw.gmin[g - 1]);  // all-ones (no value) is a NaN
+        Sig s;
+        if (g == 1) {
+            const bool imp = fmin < 1e100;
+            s.gcost = imp ? fmin : 1e100;
+            s.count = 100;  // PSO.cpp:768
+            s.topo = -1;
+        } else {
+            const Sig pv = sw.sig[g - 1];
+            const bool imp = fmin < pv.gcost;
+            s.gcost = imp ? fmin : pv.gcost;
+            s.count = imp ? 0 : pv.count + 1;
+            s.topo = pv.topo;
         }
-        sm.iscal[0] = best.i;
+        if (s.count > 0) s.topo = g;  // topology rebuilt when count > 0 (PSO.cpp:790)
+        sm.iscal[0] = s.topo;
+        if (i == 0) sw.sig[g] = s;
     }
     __syncthreads();
-    const int inf = sm.iscal[0];
-    // 3. velocity, position, check_constraints (PSO.cpp:824-842, 358-377)
+    sc.lap(0);
+    const int topo = sm.iscal[0], var = (topo == g) ? 1 : 0;
+    const double pci = sm.dscal[4];
+    // ---- informant = first argmin of pbest cost over {i} U incoming (PSO.cpp:810-812)
+    if (t >= 64 && t < 128) {
+        const int k = t - 64;
+        double v = __builtin_inf();
+        int idx = 0x7fffffff, slot = -1;
+        if (k < K) {
+            const long long tag = __double_as_longlong(ib[var][k][0]);
+            if ((tag >> 32) == (((long long)(g - 1) << 16) | topo)) {
+                v = ib[var][k][1];
+                idx = (int)(tag & 0xffffffff);
+                slot = k;
+            }
+        } else if (k == 63) {  // self (L = eye)
+            v = pci;
+            idx = i;
+        }
+        if (v != v) v = __builtin_inf();
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const double ov = __shfl_xor(v, off);
+            const int oi = __shfl_xor(idx, off), os = __shfl_xor(slot, off);
+            if (ov < v || (ov == v && oi < idx)) {
+                v = ov;
+                idx = oi;
+                slot = os;
+            }
+        }
+        if (k == 0) {
+            sm.iscal[1] = idx;
+            sm.iscal[2] = slot;
+        }
+    }
+    __syncthreads();
+    sc.lap(1);
+    const int inf = sm.iscal[1], islot = sm.iscal[2];
+    // ---- velocity, position, check_constraints (PSO.cpp:824-842, 358-377)
     const double *lb = sw.bounds, *ub = sw.bounds + HPE_DOF;
     if (t < HPE_DOF) {
-        const size_t e = (size_t)i * HPE_DOF + t;
-        const double xo = sw.x[prv][e], vo = sw.v[e], pbi = sw.pb[prv][e];
-        const double rp = philox_u01(sw.seed, ST_RP, g, i, t);
         double vn;
         if (inf == i) {
             vn = W1 * vo + (C1 * rp) * (pbi - xo);
         } else {
-            const double rg = philox_u01(sw.seed, ST_RG, g, i, t);
-            const double pbn = sw.pb[prv][(size_t)inf * HPE_DOF + t];
+            const double pbn = ib[var][islot][2 + t];
             vn = (W1 * vo + (C1 * rp) * (pbi - xo)) + (C2 * rg) * (pbn - xo);
         }
         double xn = xo + vn;
@@ -204,128 +265,269 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, DevObs o,
         if (xr < lb[t]) { xn = lb[t]; vn = 0.; }
         if (xr > ub[t]) { xn = lb[t]; vn = 0.; }  // above max -> MIN (PSO.cpp:372)
         sw.v[e] = vn;
-        sw.x[cur][e] = xn;
-        sm.th[t] = xn;
+        sw.xh[(size_t)g * P * HPE_DOF + e] = xn;
+        sm.fk.th[t] = xn;
     }
     __syncthreads();
-    // 4. evaluation and pbest (PSO.cpp:848-861)
-    const double fx = eval_block<EV_COST>(sm, o, H, nullptr);
-    const bool better = fx < pcs[i];
+    sc.lap(2);
+    // ---- evaluation and pbest (PSO.cpp:848-861)
+    const double fx = eval_block<EV_COST, HPE_NT>(sm, o, cv, H, nullptr, pre);
+    sc.start();
+    const bool better = fx < pci;
+    const double pn = better ? fx : pci;
     if (t < HPE_DOF) {
-        const size_t e = (size_t)i * HPE_DOF + t;
-        sw.pb[cur][e] = better ? sm.th[t] : sw.pb[prv][e];
+        const double row = better ? sm.fk.th[t] : pbi;
+        sw.pb[e] = row;
+        sm.fk.th[t] = row;  // the pushed pbest row
     }
-    if (t == 0) sw.pc[cur][i] = better ? fx : pcs[i];
+    if (t == 0) {
+        sw.pch[(size_t)g * P + i] = pn;
+        atomicMin(&sw.gmin[g], f64_to_bits(pn));
+    }
+    __syncthreads();
+    push_inbox(sw, g, i, topo, pn, sm.fk.th);
+    sc.lap(3);
 }
 
+// Last end-of-generation update and bestp = gbest_pos (PSO.cpp:864-882).  Replays the
+// gbest / count sequence from gmin[], finds the last improving generation g* and takes
+// particles.col(first argmin pcost) of that generation; resets gmin[] for the next call.
 __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__restrict__ out) {
     __shared__ Smem sm;
-    const int t = threadIdx.x, G = sw.G, slot = G & 1;
-    const Sig prev = (G >= 1) ? sw.sig[slot] : Sig{1e100, 100, -1};
-    bool improved;
-    int fid;
-    const Sig s = gbest_update(sm, sw, sw.pc[slot], nullptr, G, prev, &improved, &fid);
-    __syncthreads();
-    if (improved && t < HPE_DOF) sw.gpos[t] = sw.x[slot][(size_t)fid * HPE_DOF + t];
-    if (t == 0 && G >= 1 && sw.trace_g) {
-        sw.trace_g[G - 1] = s.gcost;
-        sw.trace_count[G - 1] = s.count;
-        sw.trace_topo[G - 1] = prev.topo;
+    const int t = threadIdx.x, G = sw.G, P = sw.P;
+    if (t == 0) {
+        double gcost = 1e100;
+        int last = -1, count = 100;
+        const double f0 = bits_to_f64(sw.gmin[0]);
+        if (f0 < gcost) {
+            gcost = f0;
+            last = 0;
+        }
+        for (int g = 1; g <= G; ++g) {
+            const double fm = bits_to_f64(sw.gmin[g]);
+            if (fm < gcost) {
+                gcost = fm;
+                count = 0;
+                last = g;
+            } else {
+                count += 1;
+            }
+            if (sw.trace_g) {
+                sw.trace_g[g - 1] = gcost;
+                sw.trace_count[g - 1] = count;
+                sw.trace_topo[g - 1] = sw.sig[g].topo;
+            }
+        }
+        sm.iscal[2] = last;
+        sm.dscal[5] = gcost;
     }
     __syncthreads();
-    if (t < HPE_DOF) out[t] = sw.gpos[t];  // bestp = gbest_pos (PSO.cpp:882)
-    if (t == 0) out[HPE_DOF] = s.gcost;
+    const int last = sm.iscal[2];
+    const double gcost = sm.dscal[5];
+    if (last >= 0) {
+        const double *pc = sw.pch + (size_t)last * P;
+        VI mine = {__builtin_inf(), 0};
+        for (int k = t; k < P; k += HPE_NT) {
+            const double v = nan_inf(pc[k]);
+            if (v < mine.v) {
+                mine.v = v;
+                mine.i = k;
+            }
+        }
+        const VI b = block_argmin(sm, mine);
+        if (t < HPE_DOF) out[t] = sw.xh[((size_t)last * P + b.i) * HPE_DOF + t];
+    } else if (t < HPE_DOF) {
+        out[t] = 0.0;  // gbest_pos = zeros<vec> (PSO.cpp:739) if nothing beat 1e100
+    }
+    if (t == 0) out[HPE_DOF] = gcost;
+    __syncthreads();
+    if (t < HPE_DOF) sw.gpos[t] = out[t];
+    for (int g = t; g <= G; g += HPE_NT) sw.gmin[g] = ~0ull;
 }
 
 // ------------------------------------------------------------------ refine
-// refine_init_pose (PSO.cpp:216-266) with cal_grad (:183-214) and goldstein (:438-480),
-// all in one workgroup: every thread evaluates the same scalar control flow from LDS.
-struct RefineSmem {
+// refine_init_pose (PSO.cpp:216-266) with cal_grad (:183-214) and goldstein (:438-480)
+// as ONE persistent workgroup of RF_NT threads.  Each iteration:
+//   * f_k = cal_cost2(x0, matchId, true): FK by wave 0, search by all RF_NT threads;
+//   * the 6 central differences run concurrently, one wave each (frozen matchId);
+//   * the Goldstein bracket search is evaluated SPECULATIVELY: waves 0..2^D-2 evaluate the
+//     nodes of its next D-level decision tree (D = 3 at 8 waves, 4 at 16) (node n: down child 2n = Armijo fails,
+//     up child 2n+1 = Armijo holds but Goldstein fails), then every thread walks the
+//     tree with the serial algorithm's exact rules.  Identical arithmetic on identical
+//     alphas: the result, the step tk and the evaluation count equal the serial ones.
+// Control flow is uniform: every thread evaluates the same scalar decisions from LDS.
+#ifndef RF_NT
+#define RF_NT 512
+#endif
+#define RF_NW (RF_NT / 64)
+#define RF_DEPTH (RF_NW >= 16 ? 4 : 3)  // speculated Goldstein levels per round
+#define RF_STAGE_MAX 2048  // clouds up to this size are staged in LDS with their matchId
+
+struct __align__(16) RefineSm {
+    FkSm w[RF_NW];
+    FkSm base;  // spheres of the current x0
+    double red[16][4];
     double x0[32], g[32], p[32];
+    double f[RF_NW];
 };
 
-__device__ __forceinline__ double acc2(const double *x, int n) {  // arrayops::accumulate
-    double a1 = 0, a2 = 0;
-    int i, j;
-    for (i = 0, j = 1; j < n; i += 2, j += 2) {
-        a1 += x[i];
-        a2 += x[j];
-    }
-    if (i < n) a1 += x[i];
-    return a1 + a2;
+// Goldstein bracket update (PSO.cpp:459-474), shared by the speculating waves and the walk.
+__device__ __forceinline__ void gold_up(double &a, double b, double &alpha) {
+    a = alpha;
+    const double up = 2 * alpha, mid = 0.5 * (alpha + b);
+    alpha = (mid < up) ? mid : up;  // std::min(t*alpha, 0.5*(alpha+b))
+}
+__device__ __forceinline__ void gold_down(double a, double &b, double &alpha) {
+    b = alpha;
+    alpha = 0.5 * (a + alpha);
 }
 
-__global__ __launch_bounds__(HPE_NT) void k_refine(double *__restrict__ x0g, DevObs o,
-                                                   const DevHand *__restrict__ H,
-                                                   int32_t *__restrict__ match,
-                                                   int *__restrict__ evals_out) {
-    __shared__ Smem sm;
-    __shared__ RefineSmem rs;
-    const int t = threadIdx.x;
+template <bool STAGED>
+__global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, DevObs o,
+                                                  const DevHand *__restrict__ Hg,
+                                                  int32_t *__restrict__ match_g,
+                                                  int *__restrict__ evals_out) {
+    extern __shared__ __align__(16) unsigned char dyn[];  // staged cloud + matchId
+    __shared__ RefineSm rs;
+    __shared__ DevHand hs;  // hand constants in LDS: keeps them out of the loop's registers
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    for (int q = t; q < (int)(sizeof(DevHand) / 8); q += RF_NT)
+        ((double *)&hs)[q] = ((const double *)Hg)[q];
+    const DevHand *__restrict__ H = &hs;
+    CloudView cv = obs_cloud(o);
+    int32_t *match = match_g;
+    if (STAGED) {
+        double *cx = (double *)dyn, *cy = cx + o.n, *cz = cy + o.n;
+        for (int p = t; p < o.n; p += RF_NT) {
+            cx[p] = o.cx[p];
+            cy[p] = o.cy[p];
+            cz[p] = o.cz[p];
+        }
+        cv = CloudView{cx, cy, cz, o.n};
+        match = (int32_t *)(cz + o.n);
+    }
     if (t < HPE_DOF) rs.x0[t] = x0g[t];
     __syncthreads();
+    StampClock sc;
+    sc.start();
     int evals = 0;
+    bool base_valid = false;
+    const double e = 1e-5;  // cal_grad step (PSO.cpp:195)
     for (int blk = 0; blk < 2; ++blk) {
-        const int lo = 3 * blk, hi = 3 * blk + 2;
+        const int lo = 3 * blk, hi = 3 * blk + 2;  // start_idx/end_idx (PSO.cpp:226-227)
         double tol = 1;
         int cnt = 0, iter = 0;
         while (tol > 1e-6 && iter < 15 && cnt < 1) {
-            if (t < HPE_DOF) sm.th[t] = rs.x0[t];
-            __syncthreads();
-            const double fk = eval_block<EV_COST2_CORR>(sm, o, H, match);
-            ++evals;
-            __syncthreads();  // match[] visible to the whole block
-            for (int d = lo; d <= hi; ++d) {
-                const double e = 1e-5;
-                if (t < HPE_DOF) sm.th[t] = rs.x0[t] + ((t == d) ? e : 0.0);
+            // f_k = cal_cost2(x0, matchId, true).  The spheres of x0 are already in rs.base
+            // when x0 is the accepted Goldstein point of the previous iteration
+            // (x0 + tk*p == x0 - tk*g bitwise) or an unchanged x0.
+            if (!base_valid) {
+                if (t < HPE_DOF) rs.base.th[t] = rs.x0[t];
                 __syncthreads();
-                const double fp = eval_block<EV_COST2_FROZEN>(sm, o, H, match);
-                if (t < HPE_DOF) sm.th[t] = (t == d) ? rs.x0[t] - e : rs.x0[t];
+                if (w == 0) fk_wave(rs.base, H);
                 __syncthreads();
-                const double fm = eval_block<EV_COST2_FROZEN>(sm, o, H, match);
-                evals += 2;
-                if (t == 0) rs.g[d] = (fp - fm) / (2 * e);
             }
-            if (t < HPE_DOF && (t < lo || t > hi)) rs.g[t] = 0;
+            double dep = (t < HPE_NS) ? depth_term(rs.base, t, o, H) : 0.0;
+            double al = search_align<RF_NT, true>(rs.base, cv, H, match, load_pt(cv, t));
+            double co = (t < 144) ? collide_term(rs.base, t, H) : 0.0;
+            block_sum3<RF_NT>(rs.red, al, dep, co);  // also publishes matchId to the block
+            const double fk = (al * o.lambda + dep) + co;
+            ++evals;
+            sc.lap(20);
+            // cal_grad: x0 +/- e along the 3 block dims, one wave per evaluation
+            if (w < 6) {
+                const int d = lo + (w >> 1);
+                if (l < HPE_DOF)
+                    rs.w[w].th[l] = (l == d) ? ((w & 1) ? rs.x0[l] - e : rs.x0[l] + e) : rs.x0[l];
+                wave_sync();
+                const double f = eval_wave_frozen(rs.w[w], o, cv, H, match);
+                if (l == 0) rs.f[w] = f;
+            }
             __syncthreads();
-            if (t < HPE_DOF) rs.p[t] = -1 * rs.g[t];
+            evals += 6;
+            if (t < HPE_DOF) {
+                const double g = (t >= lo && t <= hi)
+                                     ? (rs.f[2 * (t - lo)] - rs.f[2 * (t - lo) + 1]) / (2 * e)
+                                     : 0.0;
+                rs.g[t] = g;
+                rs.p[t] = -1 * g;
+            }
             __syncthreads();
-            // direct_dot_arma: two interleaved accumulators
-            double v1 = 0, v2 = 0;
+            sc.lap(21);
+            double v1 = 0, v2 = 0;  // op_dot::direct_dot_arma (two accumulators)
             for (int a = 0, b = 1; b < HPE_DOF; a += 2, b += 2) {
                 v1 += rs.g[a] * rs.p[a];
                 v2 += rs.g[b] * rs.p[b];
             }
             const double gp = v1 + v2;
+            // goldstein(x0, grad, matchId, f_k, optfunc, tk, 30)
             double A = 0, B = 1e100, alpha = 0.5, tk = 0;
-            for (int it = 0; it < 30; ++it) {
-                if (t < HPE_DOF) sm.th[t] = rs.x0[t] + alpha * rs.p[t];
+            int it = 0, accepted = -1;
+            bool done = false;
+            while (!done) {
+                if (w < (1 << RF_DEPTH) - 1) {
+                    const int node = w + 1, depth = 31 - __builtin_clz(node);
+                    double a = A, b = B, al2 = alpha;
+                    for (int k = depth - 1; k >= 0; --k) {
+                        if ((node >> k) & 1) gold_up(a, b, al2);
+                        else gold_down(a, b, al2);
+                    }
+                    if (l < HPE_DOF) rs.w[w].th[l] = rs.x0[l] + al2 * rs.p[l];
+                    wave_sync();
+                    const double f = eval_wave_frozen(rs.w[w], o, cv, H, match);
+                    if (l == 0) rs.f[w] = f;
+                }
                 __syncthreads();
-                const double f1 = eval_block<EV_COST2_FROZEN>(sm, o, H, match);
-                ++evals;
-                const double armijo = fk + 0.25 * alpha * gp;
-                const double gold = fk + (1 - 0.25) * alpha * gp;
-                if (f1 <= armijo) {
-                    if (f1 >= gold) {
-                        tk = alpha;
+                int node = 1;
+                accepted = -1;
+                for (int lev = 0; lev < RF_DEPTH && !done; ++lev) {
+                    if (it >= 30) {
+                        done = true;
+                        tk = 0;
                         break;
                     }
-                    A = alpha;
-                    const double up = 2 * alpha, mid = 0.5 * (alpha + B);
-                    alpha = (mid < up) ? mid : up;
-                } else {
-                    B = alpha;
-                    alpha = 0.5 * (A + alpha);
+                    ++it;
+                    const double f1 = rs.f[node - 1];
+                    const double armijo = fk + 0.25 * alpha * gp;
+                    const double gold = fk + (1 - 0.25) * alpha * gp;
+                    if (f1 <= armijo) {
+                        if (f1 >= gold) {
+                            tk = alpha;
+                            done = true;
+                            accepted = node - 1;
+                        } else {
+                            gold_up(A, B, alpha);
+                            node = 2 * node + 1;
+                        }
+                    } else {
+                        gold_down(A, B, alpha);
+                        node = 2 * node;
+                    }
                 }
+                if (!done && it >= 30) done = true;  // tk stays 0
+                if (done && accepted >= 0) {  // keep the accepted node's spheres for f_k
+                    for (int q = t; q < (int)(offsetof(FkSm, J) / 8); q += RF_NT)
+                        ((double *)&rs.base)[q] = ((const double *)&rs.w[accepted])[q];
+                }
+                __syncthreads();
             }
+            evals += it;
+            sc.lap(22);
             if (tk == 0) cnt += 1;
-            __syncthreads();
-            if (t < HPE_DOF) rs.x0[t] = rs.x0[t] - tk * rs.g[t];
-            double g2[HPE_DOF];
-            for (int d = 0; d < HPE_DOF; ++d) g2[d] = rs.g[d] * rs.g[d];
-            tol = sqrt(acc2(g2, HPE_DOF));
+            {  // tol = sqrt(sum(grad % grad)): arrayops::accumulate over the squares
+                double a1 = 0, a2 = 0;
+                for (int a = 0, b = 1; b < HPE_DOF; a += 2, b += 2) {
+                    a1 += rs.g[a] * rs.g[a];
+                    a2 += rs.g[b] * rs.g[b];
+                }
+                tol = sqrt(a1 + a2);
+            }
             iter += 1;
             __syncthreads();
+            if (t < HPE_DOF) rs.x0[t] = rs.x0[t] - tk * rs.g[t];
+            base_valid = true;  // accepted node copied, or tk == 0 and x0 unchanged
+            __syncthreads();
+            sc.lap(23);
         }
     }
     if (t < HPE_DOF) x0g[t] = rs.x0[t];
@@ -361,6 +563,17 @@ __global__ void k_render(const double *__restrict__ S, const DevHand *__restrict
         }
     }
     out[pix] = (best < __builtin_inf()) ? (float)(best * 10.0) : 0.0f;
+}
+
+extern "C" int hpe_debug_stamps(unsigned long long *out64) {
+    if (!out64) return HPE_E_ARG;
+    if (hipMemcpyFromSymbol(out64, HIP_SYMBOL(hpe_stamps), sizeof(unsigned long long) * 64, 0,
+                            hipMemcpyDeviceToHost) != hipSuccess)
+        return HPE_E_HIP;
+    unsigned long long z[64] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(hpe_stamps), z, sizeof(z), 0, hipMemcpyHostToDevice) != hipSuccess)
+        return HPE_E_HIP;
+    return HPE_STAMPS;
 }
 
 #include "hpe_api.inc"

@@ -17,6 +17,9 @@ struct DevHand {
     double L[5][4];                       // segment lengths (cm)
     double twc[5], tws[5];                // twist of the 2nd DH factor (thumb pCMC; fingers 1, 0)
     double radii[HPE_NS];
+    // sphere s = wa[s] * joint[a] + wb[s] * joint[a+1] of digit dg[s] (buildSpheres)
+    double wa[HPE_NS], wb[HPE_NS];
+    int32_t dg[HPE_NS], ja[HPE_NS];
 };
 
 // One preprocessed frame (device pointers), passed by value as a kernel argument.
@@ -36,19 +39,28 @@ struct Sig {  // swarm scalars carried across generation kernels
     int topo;
 };
 
-// PSO swarm state; ping-pong slots [g & 1] for everything another workgroup reads.
+// PSO swarm state.  Positions and pbest costs keep one slot per generation (history:
+// the gbest position is resolved once, in the final kernel).  Informant data travels
+// by PUSH: at the end of generation g every particle writes {tag g, pbest cost, pbest
+// row} into the inbox slots of the particles it informs under both possible
+// topologies of generation g+1 (rebuilt at g+1, or kept), so generation g+1 reads all
+// it needs from its own inbox in one round trip.
+#define IB_FIELDS 28  // tag, pbest cost, pbest position[26]
 struct DevSwarm {
-    double *x[2], *pb[2], *pc[2];
-    double *v;
-    double *gpos;
-    Sig *sig;                 // [2]
+    double *xh;               // (G+1) x P x 26   particle positions per generation
+    double *pch;              // (G+1) x P        pbest costs per generation
+    double *pb;               // P x 26           pbest positions (own particle only)
+    double *v;                // P x 26           velocities (own particle only)
+    double *inbox;            // 2 x 2 x P x K x IB_FIELDS  [g&1][kept, rebuilt][receiver][slot]
+    unsigned long long *gmin; // G+1              min pbest cost bits per generation (atomicMin)
+    Sig *sig;                 // G+1              gbest cost / count / topology per generation
     const double *normals;    // P x 26
-    const int *in_off;        // (G+1) x (P+1): incoming-link CSR per topology generation
-    const int *in_src;        // (G+1) x 3P
-    const double *bounds;     // lb[26], ub[26], std[26], x0[26]
+    const int *outl;          // (G+1) x P x 3 x 2  (receiver, slot) of each link per topology
+    const double *bounds;     // lb[26], ub[26], std[26]
+    double *gpos;             // 26               gbest position (final)
     double *trace_g;          // [G]
     int *trace_count, *trace_topo;
     uint64_t seed;
-    int P, G;
+    int P, G, K;
 };
 

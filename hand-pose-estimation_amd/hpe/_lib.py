@@ -60,6 +60,7 @@ SIGNATURES = {
     "hpe_profile_enable": (C.c_int, [C.c_void_p, C.c_int]),
     "hpe_profile_read": (C.c_int, [C.c_void_p, ip, dp, dp, dp]),
     "hpe_render_depth": (C.c_int, [C.c_void_p, dp, C.c_double, fp]),
+    "hpe_debug_stamps": (C.c_int, [C.POINTER(C.c_uint64)]),
 }
 
 _lib = None

@@ -150,6 +150,11 @@ int hpe_profile_enable(hpe_ctx *ctx, int on);
 int hpe_profile_read(hpe_ctx *ctx, int32_t *launches, double *total_ms, double *min_ms,
                      double *max_ms);
 
+/* Diagnostic build only (libhpe_stamps.so): per-phase shader-clock cycle sums
+ * [0..31] and lap counts [32..63] of block 0, reset on read.  Returns 1 in the
+ * stamps build, 0 in the product build (all zeros). */
+int hpe_debug_stamps(unsigned long long *out64);
+
 /* Synthetic 240x320 depth (float mm, zero background) of the 48-sphere model at
  * pose theta: front-most ray/sphere hit per pixel centre under K(focal).  Bench /
  * test input generator (no MSRA data on the box). */

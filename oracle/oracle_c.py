@@ -10,7 +10,7 @@ from pathlib import Path
 
 import numpy as np
 
-ORACLE_DIR = Path(__file__).resolve().parent.parent / "oracle"
+ORACLE_DIR = Path(__file__).resolve().parent
 LIB = ORACLE_DIR / "liboracle_hpe.so"
 
 dp = C.POINTER(C.c_double)
