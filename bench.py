@@ -128,6 +128,7 @@ def main():
     import torch.distributed as dist
     import hpe
     from hpe import synth
+    from hpe.dist import exchange_best, subswarm_seed
 
     torch.cuda.set_device(local)
     if world > 1:
@@ -143,7 +144,7 @@ def main():
     ctx.check(lib.hpe_set_pso_params(ctx.h, hpe._lib.ptr(ub, C.c_double),
                                      hpe._lib.ptr(lb, C.c_double), hpe._lib.ptr(sd, C.c_double),
                                      0.7298, 1.49618, 1.49618, G + 1, 1e-8, 1e-8))
-    ctx.check(lib.hpe_set_seed(ctx.h, C.c_uint64(1000 + rank)))
+    ctx.check(lib.hpe_set_seed(ctx.h, C.c_uint64(subswarm_seed(rank))))
     state = torch.zeros(27, dtype=torch.float64, device=f"cuda:{local}")
     state[:26] = torch.from_numpy(poses[0])
     torch.cuda.synchronize()
@@ -156,9 +157,7 @@ def main():
         ctx.check(lib.hpe_track_frame_dev(ctx.h, P, refine, C.c_void_p(state.data_ptr())))
         if world > 1:  # best-of-N exchange on the tracker's own stream (no host sync)
             with torch.cuda.stream(ext):
-                dist.all_gather_into_tensor(gathered, state)
-                g = gathered.view(world, 27)
-                state.copy_(g[torch.argmin(g[:, 26])])
+                exchange_best(state, gathered)
 
     for f in range(args.warmup):
         step(f)
@@ -180,8 +179,14 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    nl = C.c_int32(0); tot = C.c_double(0); mn = C.c_double(0); mx = C.c_double(0)
-    ctx.check(lib.hpe_profile_read(ctx.h, C.byref(nl), C.byref(tot), C.byref(mn), C.byref(mx)))
+    prof = {}
+    for name, kid in (("k_pso_gen", 0), ("k_refine", 1), ("k_pso_init", 2), ("k_pso_final", 3)):
+        nl = C.c_int32(0); tot = C.c_double(0); mn = C.c_double(0); mx = C.c_double(0)
+        ctx.check(lib.hpe_profile_read_kernel(ctx.h, kid, C.byref(nl), C.byref(tot),
+                                              C.byref(mn), C.byref(mx)))
+        prof[name] = {"launches": nl.value, "avg_us": tot.value / max(nl.value, 1) * 1e3,
+                      "min_us": mn.value * 1e3, "max_us": mx.value * 1e3,
+                      "total_ms": tot.value}
     ctx.check(lib.hpe_profile_enable(ctx.h, 0))
     final = state.cpu().numpy()
 
@@ -192,10 +197,12 @@ def main():
         return
     n_pts = sizes[args.warmup]
     evals = P * (G + 1) * args.steps * world
-    avg_ms = tot.value / max(nl.value, 1)
+    pg = prof["k_pso_gen"]
+    avg_s = pg["avg_us"] * 1e-6
     bytes_launch = P * algorithmic_bytes_per_eval(n_pts)
     flops_launch = P * algorithmic_flops_per_eval(n_pts)
-    achieved = bytes_launch / (avg_ms * 1e-3) / 1e9 if nl.value else None
+    achieved = bytes_launch / avg_s / 1e9 if pg["launches"] else None
+    valu = flops_launch / avg_s / 1e12 if pg["launches"] else None
     line = {
         "metric": "particle-evals/sec + tracked FPS, 320x240 depth, 256p x 30gen",
         "value": evals / el,
@@ -221,14 +228,16 @@ def main():
             "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS if achieved else None,
             "traffic": load_pmc(P, n_pts),
-            "avg_launch_us": avg_ms * 1e3, "launches": nl.value,
-            "min_launch_us": mn.value * 1e3, "max_launch_us": mx.value * 1e3,
+            "avg_launch_us": pg["avg_us"], "launches": pg["launches"],
             "bytes_per_launch": bytes_launch,
-            "valu_tflops": flops_launch / (avg_ms * 1e-3) / 1e12 if nl.value else None,
-            "valu_frac": flops_launch / (avg_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS
-            if nl.value else None,
-            "note": "algorithmic bytes per launch = P*(24N + 2048); the fp32 search is "
-                    "VALU-bound, see valu_frac (DESIGN.md §5)"},
+            "flops_per_launch": flops_launch,
+            "valu_tflops": valu,
+            "valu_frac": valu / FP32_PEAK_TFLOPS if valu else None,
+            "note": "algorithmic bytes per launch = P*(24N + 2048), per-launch time from "
+                    "hipExtLaunchKernel events on the tracker stream; the generation is "
+                    "latency-bound (one particle per workgroup, 31 dependent launches per "
+                    "frame), DESIGN.md §5"},
+        "kernels": prof,
     }
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args, sizes)

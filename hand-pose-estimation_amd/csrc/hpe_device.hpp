@@ -408,14 +408,17 @@ __device__ __forceinline__ CloudView obs_cloud(const DevObs &o) {
 // Whole-block evaluation of the particle in sm.fk.th (wave 0 does FK, NT threads the
 // search).  Every thread returns the total; terms (align, depth, collision) go to
 // sm.dscal[0..2].
-template <int MODE, int NT>
+// FK = false: the caller has already placed the centres in sm.fk.S / Sf (hpe_eval_spheres).
+template <int MODE, int NT, bool FK = true>
 __device__ __forceinline__ double eval_block(Smem &sm, const DevObs &o, const CloudView &cv,
                                              const DevHand *__restrict__ H,
                                              int32_t *__restrict__ match, Pt pre) {
     StampClock sc;
     sc.start();
-    if (threadIdx.x < 64) fk_wave(sm.fk, H);
-    __syncthreads();
+    if (FK) {
+        if (threadIdx.x < 64) fk_wave(sm.fk, H);
+        __syncthreads();
+    }
     sc.lap(10);
     const int t = threadIdx.x;
     // issue the depth gathers first: their latency hides under the search

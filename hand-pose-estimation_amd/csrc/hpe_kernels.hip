@@ -43,10 +43,11 @@ __global__ __launch_bounds__(HPE_NT) void k_build(const double *__restrict__ the
 
 template <int MODE>
 __global__ __launch_bounds__(HPE_NT) void k_eval(const double *__restrict__ theta, int P,
-                                                 DevObs o, const DevHand *__restrict__ Hg,
+                                                 const DevObs *__restrict__ og, const DevHand *__restrict__ Hg,
                                                  double *__restrict__ cost,
                                                  int32_t *__restrict__ match,
                                                  double *__restrict__ terms) {
+    const DevObs o = *og;  // the selected frame (device-resident: graph-stable args)
     __shared__ Smem sm;
     const int i = blockIdx.x, t = threadIdx.x;
     stage_hand<HPE_NT>(sm.hand, Hg);
@@ -64,6 +65,36 @@ __global__ __launch_bounds__(HPE_NT) void k_eval(const double *__restrict__ thet
             terms[3 * i + 1] = sm.dscal[1];
             terms[3 * i + 2] = sm.dscal[2];
         }
+    }
+}
+
+// Cost terms for caller-supplied sphere centres (costfunc::align_models, depth_penalty,
+// self_collision_penalty and compute_correspondences take a sphere matrix, not a theta:
+// costfunc.cpp:130-377).  S: P x 48 x 3 row-major, y/z already negated.
+template <int MODE>
+__global__ __launch_bounds__(HPE_NT) void k_eval_spheres(const double *__restrict__ S, int P,
+                                                         const DevObs *__restrict__ og, const DevHand *__restrict__ Hg,
+                                                         int32_t *__restrict__ match,
+                                                         double *__restrict__ terms) {
+    const DevObs o = *og;  // the selected frame (device-resident: graph-stable args)
+    __shared__ Smem sm;
+    const int i = blockIdx.x, t = threadIdx.x;
+    stage_hand<HPE_NT>(sm.hand, Hg);
+    const DevHand *__restrict__ H = &sm.hand;
+    if (t < 3 * HPE_NS) {
+        const int s = t / 3, r = t - 3 * s;
+        const double v = S[(size_t)i * 3 * HPE_NS + t];
+        sm.fk.S[s][r] = v;
+        ((float *)&sm.fk.Sf[s])[r] = (float)v;
+    }
+    const CloudView cv = obs_cloud(o);
+    const Pt pre = load_pt(cv, t);
+    __syncthreads();
+    eval_block<MODE, HPE_NT, false>(sm, o, cv, H, match + (size_t)i * o.n, pre);
+    if (t == 0) {
+        terms[3 * i + 0] = sm.dscal[0];
+        terms[3 * i + 1] = sm.dscal[1];
+        terms[3 * i + 2] = sm.dscal[2];
     }
 }
 
@@ -133,7 +164,8 @@ __device__ __forceinline__ void push_inbox(const DevSwarm &sw, int g, int s, int
 }
 
 __global__ __launch_bounds__(HPE_NT) void k_pso_init(DevSwarm sw, const double *__restrict__ x0,
-                                                     DevObs o, const DevHand *__restrict__ Hg) {
+                                                     const DevObs *__restrict__ og, const DevHand *__restrict__ Hg) {
+    const DevObs o = *og;  // the selected frame (device-resident: graph-stable args)
     __shared__ Smem sm;
     const int i = blockIdx.x, t = threadIdx.x;
     stage_hand<HPE_NT>(sm.hand, Hg);
@@ -160,9 +192,10 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_init(DevSwarm sw, const double *
 
 // One fused generation g >= 1 (PSO.cpp:781-879).  Round 1 loads everything: own state,
 // sig[g-1] / gmin[g-1] (previous generation's gbest bookkeeping) and the two inboxes.
-__global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, DevObs o,
+__global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *__restrict__ og,
                                                     const DevHand *__restrict__ Hg, int g,
                                                     double W1, double C1, double C2) {
+    const DevObs o = *og;  // the selected frame (device-resident: graph-stable args)
     __shared__ Smem sm;
     __shared__ double ib[2][IB_KMAX][IB_FIELDS];
     const int i = blockIdx.x, t = threadIdx.x, P = sw.P, K = sw.K;
@@ -383,10 +416,11 @@ __device__ __forceinline__ void gold_down(double a, double &b, double &alpha) {
 }
 
 template <bool STAGED>
-__global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, DevObs o,
+__global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, const DevObs *__restrict__ og,
                                                   const DevHand *__restrict__ Hg,
                                                   int32_t *__restrict__ match_g,
                                                   int *__restrict__ evals_out) {
+    const DevObs o = *og;  // the selected frame (device-resident: graph-stable args)
     extern __shared__ __align__(16) unsigned char dyn[];  // staged cloud + matchId
     __shared__ RefineSm rs;
     __shared__ DevHand hs;  // hand constants in LDS: keeps them out of the loop's registers

@@ -6,6 +6,7 @@
 #define HPE_NT 512
 #define HPE_NW (HPE_NT / 64)
 #define HPE_NS 48
+#define HPE_MAX_SLOTS 4096  // resident frames per context
 #define HPE_DOF 26
 #define HPE_IMG_H 240
 #define HPE_IMG_W 320

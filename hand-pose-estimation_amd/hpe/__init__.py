@@ -253,9 +253,48 @@ class costfunc:
         self.last_terms = terms
         return cost.value
 
-    def compute_correspondences(self, theta):
-        """matchId of theta's spheres for every cloud point (BFMatcher semantics)."""
-        return self.cal_cost_batch(np.asarray(theta).reshape(1, 26), return_match=True)[1][0]
+    # ---- term-level API on a sphere matrix (costfunc.cpp:130-377), one launch each
+    def _sphere_terms(self, spheres, matchId=None):
+        self._sync_frame()
+        S = _lib.as_f64(spheres, (48, 3))
+        n = len(self.observation.get_ptncloud())
+        corr = matchId is None
+        m = np.zeros(n, dtype=np.int32) if corr else np.ascontiguousarray(matchId, dtype=np.int32)
+        terms = np.zeros(3)
+        self.ctx.check(self.ctx.lib.hpe_eval_spheres(self.ctx.h, ptr(S, C.c_double), 1, int(corr),
+                                                     ptr(m, C.c_int32), ptr(terms, C.c_double)))
+        return terms, m
+
+    def _same_cloud(self, ptncloud):
+        own = self.observation.get_ptncloud()
+        if ptncloud is not own and not np.array_equal(np.asarray(ptncloud), own):
+            raise ValueError("the device path evaluates the observation's own point cloud")
+
+    def compute_correspondences(self, ptns, sphM, matchId):
+        """costfunc.cpp:306-343: nearest sphere centre per cloud point (BFMatcher, fp32,
+        first index on ties).  matchId (int32, len N) is filled in place."""
+        self._same_cloud(ptns)
+        _, m = self._sphere_terms(sphM)
+        matchId[...] = m
+        return matchId
+
+    def align_models(self, spheresR, spheresM, ptncloud, matchId):
+        """costfunc.cpp:346-377: (48/N) sum (|p - S[m]| - r[m])^2 with the given matchId."""
+        self._same_cloud(ptncloud)
+        if not np.array_equal(np.asarray(spheresR, dtype=np.float64), self.hand.spheres_radii):
+            raise ValueError("the device path uses the hand's own radii")
+        return float(self._sphere_terms(spheresM, matchId)[0][0])
+
+    def depth_penalty(self, cam_mat, depthmp, spheres, disttrans, scale):
+        """costfunc.cpp:227-304 on the observation's depth / DT / scale.  Like the
+        reference it un-negates y and z of `spheres` in place (:249)."""
+        val = float(self._sphere_terms(spheres)[0][1])
+        spheres[:, 1:3] *= -1
+        return val
+
+    def self_collision_penalty(self, spheresM, spheresR):
+        """costfunc.cpp:130-197: adjacent-digit sphere overlap penalty."""
+        return float(self._sphere_terms(spheresM)[0][2])
 
 
 class PSO:

@@ -14,6 +14,7 @@ import numpy as np
 PKG_DIR = Path(__file__).resolve().parent.parent  # hand-pose-estimation_amd/
 LIB_PATH = PKG_DIR / "libhpe.so"
 
+PROF_PSO_GEN, PROF_REFINE, PROF_PSO_INIT, PROF_PSO_FINAL = 0, 1, 2, 3
 HPE_OK, HPE_E_ARG, HPE_E_HIP, HPE_E_STATE, HPE_E_NOMEM, HPE_E_NODEVICE = 0, -1, -2, -3, -4, -5
 
 dp = C.POINTER(C.c_double)
@@ -49,6 +50,7 @@ SIGNATURES = {
     "hpe_build_spheres": (C.c_int, [C.c_void_p, dp, C.c_int, dp, dp]),
     "hpe_eval_costs": (C.c_int, [C.c_void_p, dp, C.c_int, C.c_int, dp, ip]),
     "hpe_cal_cost2": (C.c_int, [C.c_void_p, dp, ip, C.c_int, dp, dp]),
+    "hpe_eval_spheres": (C.c_int, [C.c_void_p, dp, C.c_int, C.c_int, ip, dp]),
     "hpe_set_pso_params": (C.c_int, [C.c_void_p, dp, dp, dp, C.c_double, C.c_double,
                                      C.c_double, C.c_int, C.c_double, C.c_double]),
     "hpe_set_seed": (C.c_int, [C.c_void_p, C.c_uint64]),
@@ -59,6 +61,7 @@ SIGNATURES = {
     "hpe_track_frame_dev": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
     "hpe_profile_enable": (C.c_int, [C.c_void_p, C.c_int]),
     "hpe_profile_read": (C.c_int, [C.c_void_p, ip, dp, dp, dp]),
+    "hpe_profile_read_kernel": (C.c_int, [C.c_void_p, C.c_int, ip, dp, dp, dp]),
     "hpe_render_depth": (C.c_int, [C.c_void_p, dp, C.c_double, fp]),
     "hpe_debug_stamps": (C.c_int, [C.POINTER(C.c_uint64)]),
 }

@@ -111,6 +111,15 @@ int hpe_eval_costs(hpe_ctx *ctx, const double *theta, int P, int with_collision,
 int hpe_cal_cost2(hpe_ctx *ctx, const double theta[26], int32_t *match_inout,
                   int compute_corr, double *cost_out, double terms_out[3]);
 
+/* The cost terms for caller-supplied sphere centres: costfunc::compute_correspondences
+ * (costfunc.cpp:306-343), align_models (:346-377), depth_penalty (:227-304) and
+ * self_collision_penalty (:130-197), which take a sphere matrix rather than a theta.
+ * S: P*48*3 (row-major per particle, y/z negated as build_hand_model returns them).
+ * match_inout: P*n int32, written when compute_corr != 0, read otherwise.
+ * terms_out: P*3 {align, depth, collision}. */
+int hpe_eval_spheres(hpe_ctx *ctx, const double *S, int P, int compute_corr,
+                     int32_t *match_inout, double *terms_out);
+
 /* PSO::set_pso_params (PSO.cpp:38-54).  omega/phip/phig/minstep/minfunc are kept
  * for API parity; pso_evolve uses the SPSO-2011 constants (PSO.cpp:772-774). */
 int hpe_set_pso_params(hpe_ctx *ctx, const double ub[26], const double lb[26],
@@ -143,12 +152,22 @@ int hpe_track_frame(hpe_ctx *ctx, int num_p, int refine, double x0_inout[26],
 int hpe_track_frame_dev(hpe_ctx *ctx, int num_p, int refine, double *d_state);
 
 /* Kernel timing with HIP events on the context stream (bench instrumentation).
- * While enabled, every launch of the fused generation kernel (k_pso_gen) is
- * bracketed by an event pair; hpe_profile_read synchronises and returns the count and
- * total/min/max device milliseconds since the last enable. */
+ * While enabled, every dispatch of the profiled kernels is launched through
+ * hipExtLaunchKernel with a start/stop event pair (dispatch-packet timestamps: the
+ * kernel's own execution interval, as rocprofv3 --kernel-trace reports it).
+ * hpe_profile_read_kernel synchronises and returns the launch count and total/min/max
+ * device milliseconds of one kernel since the last enable; hpe_profile_read is
+ * hpe_profile_read_kernel(HPE_PROF_PSO_GEN). */
+#define HPE_PROF_PSO_GEN 0   /* k_pso_gen: one fused PSO generation */
+#define HPE_PROF_REFINE 1    /* k_refine: refine_init_pose */
+#define HPE_PROF_PSO_INIT 2  /* k_pso_init */
+#define HPE_PROF_PSO_FINAL 3 /* k_pso_final */
+#define HPE_PROF_KERNELS 4
 int hpe_profile_enable(hpe_ctx *ctx, int on);
 int hpe_profile_read(hpe_ctx *ctx, int32_t *launches, double *total_ms, double *min_ms,
                      double *max_ms);
+int hpe_profile_read_kernel(hpe_ctx *ctx, int kernel, int32_t *launches, double *total_ms,
+                            double *min_ms, double *max_ms);
 
 /* Diagnostic build only (libhpe_stamps.so): per-phase shader-clock cycle sums
  * [0..31] and lap counts [32..63] of block 0, reset on read.  Returns 1 in the

@@ -1,0 +1,85 @@
+"""Multi-rank path on the CPU (gloo, world_size 2): the per-frame best-of-subswarms
+exchange of hpe.dist (the code bench.py runs over RCCL), with the subswarms computed by
+the C oracle so the expected winner is known independently.  SURVEY.md §8e."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import hand_data
+import oracle_np
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _subswarm(rank, frames_seed=31, P=8, maxiter=3):
+    import oracle_c
+    from hpe.dist import subswarm_seed
+    o = oracle_c.load(build=False)
+    geo, rad = hand_data.geometry_cm()
+    h = o.hand(geo, rad)
+    nh = oracle_np.Hand(geo, rad)
+    poses = hand_data.trajectory(2, seed=frames_seed)
+    obs = o.preprocess(oracle_np.render_depth_mm(nh, poses[1]))
+    ub, lb, sd = oracle_np.reference_bounds()
+    bp, bc, _ = o.pso_evolve(h, obs, poses[0], P, maxiter, lb, ub, sd, seed=subswarm_seed(rank),
+                             nthreads=1)
+    return np.concatenate([bp, [bc]])
+
+
+def _worker(rank, world, port, out_dir, mode):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from hpe.dist import exchange_best
+    if mode == "pso":
+        st = torch.from_numpy(_subswarm(rank))
+    elif mode == "tie":
+        st = torch.full((27,), float(rank), dtype=torch.float64)
+        st[26] = 5.0
+    else:  # nan: rank 0 diverged
+        st = torch.full((27,), float(rank), dtype=torch.float64)
+        st[26] = float("nan") if rank == 0 else 7.0
+    exchange_best(st)
+    np.save(os.path.join(out_dir, f"r{rank}.npy"), st.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run(tmp_path, mode, world=2):
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), mode), nprocs=world,
+                       join=True, start_method="spawn")
+    return [np.load(tmp_path / f"r{r}.npy") for r in range(world)]
+
+
+def test_exchange_picks_best_subswarm(tmp_path):
+    res = _run(tmp_path, "pso")
+    expect = [_subswarm(r) for r in range(2)]
+    win = int(np.argmin([e[26] for e in expect]))
+    for r in res:
+        np.testing.assert_array_equal(r, expect[win])
+    assert expect[0][26] != expect[1][26]  # distinct streams per rank
+
+
+def test_exchange_tie_lowest_rank(tmp_path):
+    for r in _run(tmp_path, "tie"):
+        assert r[0] == 0.0 and r[26] == 5.0
+
+
+def test_exchange_nan_never_wins(tmp_path):
+    for r in _run(tmp_path, "nan"):
+        assert r[0] == 1.0 and r[26] == 7.0
+
+
+def test_single_rank_is_identity():
+    from hpe.dist import pick_best, subswarm_seed
+    assert subswarm_seed(0) == 1000
+    g = torch.tensor([[1.0] * 26 + [3.0], [2.0] * 26 + [3.0]], dtype=torch.float64)
+    assert pick_best(g)[0] == 1.0

@@ -1,0 +1,126 @@
+"""GPU parity of the host C++ façade (hpe_facade.hpp: the reference's handmodel /
+observedmodel / costfunc / PSO names over the C ABI) and of the term-level costfunc API.
+
+hpe_track is test_full (testmodel.cpp:27-146) written against the façade: the same
+.bin frames, hand files and call sequence.  Its per-frame costs and poses must match the
+C oracle running the same sequence (tolerances as test_gpu_parity.py: pose 1e-6,
+cost relative 1e-8).
+"""
+import json
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import hand_data
+import oracle_np
+
+pytestmark = pytest.mark.gpu
+
+PKG = hand_data.ROOT / "hand-pose-estimation_amd"
+
+
+def _write_inputs(tmp_path, np_hand, poses):
+    d = json.loads(hand_data.HAND_JSON.read_text())
+    hand = tmp_path / "misc"
+    hand.mkdir()
+    (hand / "hgeo.dat").write_text("\n".join(repr(float(v)) for v in d["hgeo_mm"]) + "\n")
+    (hand / "rad.dat").write_text("\n".join(repr(float(v)) for v in d["rad_mm"]) + "\n")
+    frames = tmp_path / "Subject1"
+    frames.mkdir()
+    depth = []
+    for f, th in enumerate(poses):
+        dm = oracle_np.render_depth_mm(np_hand, th).astype(np.float32)
+        dm.tofile(frames / f"{f:06d}_depth.bin")
+        depth.append(dm)
+    return hand, frames, depth
+
+
+def _run_track(hand, frames, n, P, maxiter, fused, pose_out):
+    exe = PKG / "hpe_track"
+    assert exe.exists(), "build hand-pose-estimation_amd (make) first"
+    out = subprocess.run([str(exe), "--hand", str(hand), "--frames", str(frames), "--n", str(n),
+                          "--particles", str(P), "--maxiter", str(maxiter), "--refine", "1",
+                          "--fused", str(fused), "--pose-out", str(pose_out)],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    costs = [float(m) for m in re.findall(r"frame\d{6}-cost: (\S+)", out.stdout)]
+    assert len(costs) == n, out.stdout
+    return np.array(costs), np.loadtxt(pose_out).reshape(n, 26)
+
+
+def test_cpp_driver_matches_oracle(tmp_path, oracle, ora_hand, np_hand):
+    n, P, maxiter = 3, 32, 6
+    poses = hand_data.trajectory(n, seed=21)
+    hand, frames, depth = _write_inputs(tmp_path, np_hand, poses)
+    ub, lb, sd = oracle_np.reference_bounds()
+    x = oracle_np.X0.copy()
+    ref_c, ref_x = [], []
+    for f in range(n):
+        obs = oracle.preprocess(depth[f])
+        x, _ = oracle.refine(ora_hand, obs, x)
+        x, _, _ = oracle.pso_evolve(ora_hand, obs, x, P, maxiter, lb, ub, sd)
+        ref_c.append(oracle.cal_cost(ora_hand, obs, x))
+        ref_x.append(x.copy())
+    ref_c, ref_x = np.array(ref_c), np.array(ref_x)
+    for fused in (0, 1):
+        c, xs = _run_track(hand, frames, n, P, maxiter, fused, tmp_path / f"poses{fused}.txt")
+        np.testing.assert_allclose(xs, ref_x, rtol=0, atol=1e-6)
+        np.testing.assert_allclose(c, ref_c, rtol=1e-8, atol=0)
+
+
+def test_cpp_facade_api(tmp_path, np_hand):
+    """tests/cpp/facade_gpu.cpp drives every façade method once on the GPU and prints
+    the values; they must equal the Python mirror's (same library, same inputs)."""
+    src = hand_data.ROOT / "tests" / "cpp" / "facade_gpu.cpp"
+    exe = tmp_path / "facade_gpu"
+    subprocess.run(["g++", "-O1", "-std=c++17", "-o", str(exe), str(src),
+                    f"-I{PKG / 'facade'}", f"-L{PKG}", "-lhpe_facade", "-lhpe",
+                    f"-Wl,-rpath,{PKG}"], check=True, timeout=120)
+    hand, frames, depth = _write_inputs(tmp_path, np_hand, hand_data.trajectory(1, seed=3))
+    out = subprocess.run([str(exe), str(hand), str(frames) + "/"], capture_output=True,
+                         text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    vals = dict(l.split("=", 1) for l in out.stdout.split() if "=" in l)
+    import hpe
+    gh = hpe.reference_hand(0)
+    om = hpe.observedmodel(); om.downsample = True; om.set_depth_mm(depth[0])
+    cf = hpe.costfunc(gh, om)
+    th = oracle_np.X0 + 1.5
+    assert float(vals["cal_cost"]) == cf.cal_cost(th)
+    m = np.zeros(len(om.get_ptncloud()), np.int32)
+    assert float(vals["cal_cost2"]) == cf.cal_cost2(th, m, True)
+    S = gh.build_hand_model(th)
+    assert float(vals["S0x"]) == S[0, 0] and float(vals["S47z"]) == S[47, 2]
+    assert float(vals["align"]) == cf.align_models(gh.get_radii(), S, om.get_ptncloud(), m)
+    assert float(vals["collision"]) == cf.self_collision_penalty(S, gh.get_radii())
+    assert float(vals["depth"]) == cf.depth_penalty(None, None, S.copy(), None, 0.0)
+    assert int(vals["m_sum"]) == int(m.sum())
+
+
+def test_term_api_matches_oracle(oracle, ora_hand, np_hand):
+    """align_models / depth_penalty / self_collision_penalty / compute_correspondences on a
+    sphere matrix (costfunc.cpp:130-377) against the oracle's terms."""
+    import hpe
+    gh = hpe.reference_hand(0)
+    truth = hand_data.trajectory(2, seed=8)[1]
+    d = oracle_np.render_depth_mm(np_hand, truth)
+    obs = oracle.preprocess(d)
+    om = hpe.observedmodel(); om.downsample = True; om.set_depth_mm(d)
+    cf = hpe.costfunc(gh, om)
+    rng = np.random.default_rng(4)
+    for th in hand_data.random_thetas(rng, 6, x0=truth, spread=0.5):
+        cr, tr, mr = oracle.terms(ora_hand, obs, th)
+        S = oracle.build(ora_hand, th)
+        m = np.zeros(obs.n, np.int32)
+        cf.compute_correspondences(om.get_ptncloud(), S, m)
+        assert np.array_equal(m, mr)
+        np.testing.assert_allclose(cf.align_models(gh.get_radii(), S, om.get_ptncloud(), m),
+                                   tr[0], rtol=1e-9)
+        Sd = S.copy()
+        np.testing.assert_allclose(cf.depth_penalty(None, None, Sd, None, 0.0), tr[1],
+                                   rtol=1e-9, atol=1e-300)
+        np.testing.assert_array_equal(Sd[:, 1:], -S[:, 1:])  # un-negated like :249
+        np.testing.assert_allclose(cf.self_collision_penalty(S, gh.get_radii()), tr[2],
+                                   rtol=1e-9, atol=1e-300)

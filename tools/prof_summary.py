@@ -1,0 +1,91 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 output (rocpd SQLite .db or --output-format csv directories) into
+the files committed under profiles/:
+
+  kernel stats   name, calls, total/avg/min/max ns, % (the --kernel-trace --stats view)
+  PMC per launch average FETCH_SIZE / WRITE_SIZE (KB) per dispatch of one kernel, and the
+                 HBM traffic estimate  2 x FETCH_SIZE + WRITE_SIZE  (MI355X_MICROARCH.md,
+                 HBM section: gfx950 FETCH_SIZE counts half the bytes of wide reads)
+
+usage: prof_summary.py stats RUN_DIR OUT.csv
+       prof_summary.py pmc FETCH_DIR WRITE_DIR KERNEL P N OUT.json
+"""
+import csv
+import glob
+import json
+import os
+import sqlite3
+import sys
+from collections import defaultdict
+
+
+def _db(d):
+    f = glob.glob(os.path.join(d, "**", "*.db"), recursive=True)
+    return sqlite3.connect(f[0]) if f else None
+
+
+def kernel_rows(d):
+    """(name, duration_ns) per dispatch."""
+    c = _db(d)
+    if c is not None:
+        return [(n, float(dur)) for n, dur in c.execute("select name, duration from kernels")]
+    f = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)[0]
+    with open(f) as fh:
+        return [(r["Kernel_Name"], float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
+                for r in csv.DictReader(fh)]
+
+
+def counter_rows(d, counter):
+    """(kernel name, value) per dispatch for one counter."""
+    c = _db(d)
+    if c is not None:
+        q = "select kernel_name, value from counters_collection where counter_name = ?"
+        return [(n, float(v)) for n, v in c.execute(q, (counter,))]
+    f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
+    with open(f) as fh:
+        return [(r["Kernel_Name"], float(r["Counter_Value"])) for r in csv.DictReader(fh)
+                if r["Counter_Name"] == counter]
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "")
+
+
+def stats(run_dir, out):
+    agg = defaultdict(list)
+    for n, dur in kernel_rows(run_dir):
+        agg[short(n)].append(dur)
+    total = sum(sum(v) for v in agg.values())
+    rows = sorted(agg.items(), key=lambda kv: -sum(kv[1]))
+    with open(out, "w", newline="") as fh:
+        w = csv.writer(fh)
+        w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "MinNs", "MaxNs", "Percentage"])
+        for n, v in rows:
+            w.writerow([n, len(v), int(sum(v)), round(sum(v) / len(v), 1), int(min(v)),
+                        int(max(v)), round(100 * sum(v) / total, 2)])
+    for n, v in rows[:8]:
+        print(f"{n:32s} calls {len(v):6d} avg {sum(v) / len(v) / 1e3:9.2f} us "
+              f"{100 * sum(v) / total:6.2f} %")
+
+
+def pmc(fetch_dir, write_dir, kernel, P, N, out):
+    f = [v for n, v in counter_rows(fetch_dir, "FETCH_SIZE") if short(n) == kernel]
+    w = [v for n, v in counter_rows(write_dir, "WRITE_SIZE") if short(n) == kernel]
+    fk, wk = sum(f) / len(f), sum(w) / len(w)
+    res = {"kernel": kernel, "particles": P, "cloud_points": N,
+           "dispatches": {"fetch_pass": len(f), "write_pass": len(w)},
+           "fetch_size_kb_raw": fk, "write_size_kb": wk,
+           "bytes_per_launch": (2 * fk + wk) * 1024,
+           "correction": "2 x FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE counts half the "
+                         "bytes of wide coalesced reads; MI355X_MICROARCH.md HBM section); "
+                         "Infinity-Cache hits are counted, so this is L2-miss traffic"}
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "stats":
+        stats(sys.argv[2], sys.argv[3])
+    else:
+        pmc(sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5]), int(sys.argv[6]), sys.argv[7])
