@@ -163,13 +163,17 @@ def main():
         step(f)
     ctx.check(lib.hpe_sync(ctx.h))
     torch.cuda.synchronize()
-    ctx.check(lib.hpe_profile_enable(ctx.h, 1))
+    # timed region: graph-replayed frames; one event pair per frame on the tracker stream
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for f in range(args.warmup, n_frames):
+    for k, f in enumerate(range(args.warmup, n_frames)):
+        ev[k][0].record(ext)
         step(f)
+        ev[k][1].record(ext)
     ctx.check(lib.hpe_sync(ctx.h))
     torch.cuda.synchronize()
     if world > 1:
@@ -179,6 +183,14 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    frame_us = [a.elapsed_time(b) * 1e3 for a, b in ev]
+    final = state.cpu().numpy()
+    # per-kernel durations: the same frames once more with every dispatch bracketed by
+    # hipExtLaunchKernel start/stop events (direct launches; kernels are identical)
+    ctx.check(lib.hpe_profile_enable(ctx.h, 1))
+    for f in range(args.warmup, n_frames):
+        step(f)
+    ctx.check(lib.hpe_sync(ctx.h))
     prof = {}
     for name, kid in (("k_pso_gen", 0), ("k_refine", 1), ("k_pso_init", 2), ("k_pso_final", 3)):
         nl = C.c_int32(0); tot = C.c_double(0); mn = C.c_double(0); mx = C.c_double(0)
@@ -188,7 +200,8 @@ def main():
                       "min_us": mn.value * 1e3, "max_us": mx.value * 1e3,
                       "total_ms": tot.value}
     ctx.check(lib.hpe_profile_enable(ctx.h, 0))
-    final = state.cpu().numpy()
+    prof["frame_graph"] = {"launches": len(frame_us), "avg_us": sum(frame_us) / len(frame_us),
+                           "min_us": min(frame_us), "max_us": max(frame_us)}
 
     if rank != 0:
         if world > 1:

@@ -23,7 +23,9 @@ struct DevHand {
     int32_t dg[HPE_NS], ja[HPE_NS];
 };
 
-// One preprocessed frame (device pointers), passed by value as a kernel argument.
+// One preprocessed frame (device pointers).  Kept in HBM (one per slot + the selected
+// one); kernels take a pointer to the selected descriptor so their arguments never change
+// from frame to frame and a tracked frame replays as one hipGraph.
 struct DevObs {
     const double *cx, *cy, *cz;  // SoA cloud, n points (X, -Y, -Z) cm
     const double *depth;         // 240 x 320 cm

@@ -1,7 +1,11 @@
+# Round-1 GPU evidence: GPU tests, bench (default config), rocprofv3 kernel-trace stats of
+# the same bench command, and the two PMC passes (FETCH_SIZE, WRITE_SIZE) on k_pso_gen.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out/r01
-timeout -k 10 400 python -m pytest tests -x -q -m gpu > gpurun_out/r01/pytest_gpu.log 2>&1 && \
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r01/kt -o run -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/r01/bench_kt.log 2>&1 && \
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/r01/pmc_fetch -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/r01/pmc_fetch.log 2>&1 && \
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/r01/pmc_write -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/r01/pmc_write.log 2>&1
+O=gpurun_out/r01
+mkdir -p $O
+timeout -k 10 400 python -m pytest tests -x -q -m gpu > $O/pytest_gpu.log 2>&1 && \
+timeout -k 10 300 python bench.py > $O/bench.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 bench.py --no-cpu-baseline > $O/bench_kt.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc_fetch -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > $O/pmc_fetch.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc_write -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > $O/pmc_write.log 2>&1
