@@ -207,6 +207,33 @@ __device__ __forceinline__ double wave_sum(double v) {
     return ((readlane_f64(v, 0) + readlane_f64(v, 16)) + readlane_f64(v, 32)) +
            readlane_f64(v, 48);
 }
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
+}
+// Lexicographic (v, idx) minimum over the wave (Armadillo min(index): first minimum wins).
+// v must not be NaN.  Returns the winner's idx and payload in every lane.
+__device__ __forceinline__ void wave_argmin_lex(double v, int idx, int pay, int &out_idx,
+                                                int &out_pay) {
+    double m = v;
+    m = fmin(m, dpp_f64<0xB1>(m));
+    m = fmin(m, dpp_f64<0x4E>(m));
+    m = fmin(m, dpp_f64<0x141>(m));
+    m = fmin(m, dpp_f64<0x140>(m));
+    const double mn = fmin(fmin(readlane_f64(m, 0), readlane_f64(m, 16)),
+                           fmin(readlane_f64(m, 32), readlane_f64(m, 48)));
+    int c = (v == mn) ? idx : 0x7fffffff;
+    c = min(c, dpp_i32<0xB1>(c));
+    c = min(c, dpp_i32<0x4E>(c));
+    c = min(c, dpp_i32<0x141>(c));
+    c = min(c, dpp_i32<0x140>(c));
+    const int mi = min(min(__builtin_amdgcn_readlane(c, 0), __builtin_amdgcn_readlane(c, 16)),
+                       min(__builtin_amdgcn_readlane(c, 32), __builtin_amdgcn_readlane(c, 48)));
+    const unsigned long long b = __ballot(v == mn && idx == mi);
+    out_idx = mi;
+    out_pay = __builtin_amdgcn_readlane(pay, (int)__ffsll((long long)b) - 1);
+}
+
 // three independent sums interleaved for ILP
 __device__ __forceinline__ void wave_sum3(double &a, double &b, double &c) {
     a += dpp_f64<0xB1>(a); b += dpp_f64<0xB1>(b); c += dpp_f64<0xB1>(c);

@@ -111,12 +111,14 @@ __device__ __forceinline__ bool vi_less(VI a, VI b) {
 __device__ __forceinline__ double nan_inf(double v) { return (v != v) ? __builtin_inf() : v; }
 
 __device__ VI block_argmin(Smem &sm, VI mine) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        VI other;
-        other.v = __shfl_xor(mine.v, o);
-        other.i = __shfl_xor(mine.i, o);
-        if (vi_less(other, mine)) mine = other;
+    int wi, unused;
+    wave_argmin_lex(nan_inf(mine.v), mine.i, 0, wi, unused);
+    mine.v = nan_inf(mine.v);
+    {
+        // the winner's value: every lane holding idx wi has the minimum
+        const unsigned long long b = __ballot(mine.i == wi);
+        mine.v = readlane_f64(mine.v, (int)__ffsll((long long)b) - 1);
+        mine.i = wi;
     }
     const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
@@ -144,23 +146,30 @@ __device__ __forceinline__ size_t ib_index(const DevSwarm &sw, int par, int var,
     return ((((size_t)par * 2 + var) * sw.P + r) * sw.K + slot) * IB_FIELDS;
 }
 
-// Push {tag = (g, s), pbest cost, pbest row} of particle s after generation g into the
-// inboxes of its receivers under the topology of generation g+1 (var 1) and under the
-// kept topology topo_g (var 0).  168 lanes: 6 destinations x 28 fields.
-__device__ __forceinline__ void push_inbox(const DevSwarm &sw, int g, int s, int topo_g,
-                                           double pc, const double *row) {
-    const int t = threadIdx.x;
-    if (g >= sw.G || t >= 6 * IB_FIELDS) return;
-    const int dst = t / IB_FIELDS, fld = t - IB_FIELDS * dst, var = dst < 3 ? 1 : 0;
-    const int tt = var ? g + 1 : topo_g;
-    if (tt < 1) return;
-    const int *o = sw.outl + (((size_t)tt * sw.P + s) * 3 + (dst % 3)) * 2;
-    const int r = o[0], slot = o[1];
-    // tag = (generation, topology, sender): a slot is only valid for the exact
-    // (g, topology) the reader expects, whatever an earlier call left behind.
+// Push {tag = (g, topology, s), pbest cost, pbest row} of particle s after generation g
+// into the inboxes of its receivers under the topology of generation g+1 (var 1) and
+// under the kept topology topo_g (var 0).  Lane q in [0, 168): destination q / 28, field
+// q % 28; (r, slot) = this lane's link, prefetched by the caller (r < 0: no push).
+__device__ __forceinline__ void push_inbox(const DevSwarm &sw, int g, int s, int q, int r, int slot,
+                                           int tt, double pc, const double *row) {
+    if (r < 0) return;
+    const int dst = q / IB_FIELDS, fld = q - IB_FIELDS * dst, var = dst < 3 ? 1 : 0;
+    // the tag makes a slot valid only for the exact (g, topology) the reader expects,
+    // whatever an earlier call left behind
     const double val = (fld == 0) ? __longlong_as_double(((long long)g << 48) | ((long long)tt << 32) | s)
                        : (fld == 1) ? pc : row[fld - 2];
     sw.inbox[ib_index(sw, g & 1, var, r, slot) + fld] = val;
+}
+
+// Link of lane q of the pushing waves for topology tt (r = -1 when nothing is pushed).
+__device__ __forceinline__ void load_link(const DevSwarm &sw, int g, int s, int q, int tt, int &r,
+                                          int &slot) {
+    r = -1;
+    slot = 0;
+    if (g >= sw.G || q >= 6 * IB_FIELDS || tt < 1) return;
+    const int *o = sw.outl + (((size_t)tt * sw.P + s) * 3 + (q / IB_FIELDS) % 3) * 2;
+    r = o[0];
+    slot = o[1];
 }
 
 __global__ __launch_bounds__(HPE_NT) void k_pso_init(DevSwarm sw, const double *__restrict__ x0,
@@ -171,6 +180,10 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_init(DevSwarm sw, const double *
     stage_hand<HPE_NT>(sm.hand, Hg);
     const DevHand *__restrict__ H = &sm.hand;
     const double *sd = sw.bounds + 2 * HPE_DOF;
+    int lr, ls;  // pushing lanes: waves 1..3 (q = t - 64), topology 1 = rebuilt for gen 1
+    const int q = t - 64;
+    if (q >= 0 && q < 3 * IB_FIELDS) load_link(sw, 0, i, q, 1, lr, ls);
+    else lr = -1, ls = 0;
     if (t < HPE_DOF) {  // particles = x0 + randn % std (PSO.cpp:67-72)
         const size_t e = (size_t)i * HPE_DOF + t;
         const double x = x0[t] + sw.normals[e] * sd[t];
@@ -187,11 +200,13 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_init(DevSwarm sw, const double *
         sw.pch[i] = c;
         atomicMin(&sw.gmin[0], f64_to_bits(c));
     }
-    push_inbox(sw, 0, i, -1, c, sm.fk.th);
+    push_inbox(sw, 0, i, q, lr, ls, 1, c, sm.fk.th);
 }
 
-// One fused generation g >= 1 (PSO.cpp:781-879).  Round 1 loads everything: own state,
-// sig[g-1] / gmin[g-1] (previous generation's gbest bookkeeping) and the two inboxes.
+// One fused generation g >= 1 (PSO.cpp:781-879).  Wave 0 carries the serial part: every
+// load of the generation at once (own state, draws, sig[g-1] / gmin[g-1], both inboxes),
+// the topology decision, the informant, the velocity step and FK, with wave-level syncs
+// only.  Waves 1..3 prefetch the push links meanwhile; then all 8 waves search.
 __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *__restrict__ og,
                                                     const DevHand *__restrict__ Hg, int g,
                                                     double W1, double C1, double C2) {
@@ -203,108 +218,122 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
     const DevHand *__restrict__ H = &sm.hand;
     StampClock sc;
     sc.start();
-    // ---- round 1: every load of this generation, all independent
     const CloudView cv = obs_cloud(o);
     const Pt pre = load_pt(cv, t);  // this thread's first cloud point, used after FK
-    double xo = 0, vo = 0, pbi = 0, rp = 0, rg = 0;
     const size_t e = (size_t)i * HPE_DOF + t;
-    if (t < HPE_DOF) {
-        xo = sw.xh[(size_t)(g - 1) * P * HPE_DOF + e];
-        vo = sw.v[e];
-        pbi = sw.pb[e];
-        rp = philox_u01(sw.seed, ST_RP, g, i, t);
-        rg = philox_u01(sw.seed, ST_RG, g, i, t);
-    }
-    {
+    const int q = t - 64;  // pushing lanes (waves 1..3): var-1 links now, var-0 after the decision
+    int lr = -1, ls = 0;
+    if (q >= 0 && q < 3 * IB_FIELDS) load_link(sw, g, i, q, g + 1, lr, ls);
+    double pbi = 0, xo = 0, vo = 0, rp = 0, rg = 0;  // own state (lanes t < 26 of wave 0)
+    int inf = 0, islot = -1, var = 0;
+    if (t >= 64) {
+        // ---- waves 1..7: both informant inboxes (payload rows) into LDS, loads first
         const double *src = sw.inbox + ib_index(sw, (g - 1) & 1, 0, i, 0);
         const size_t var_stride = (size_t)P * K * IB_FIELDS;
-        for (int q = t; q < 2 * K * IB_FIELDS; q += HPE_NT) {
-            const int var = q / (K * IB_FIELDS), rem = q - var * K * IB_FIELDS;
-            (&ib[var][0][0])[rem] = src[var * var_stride + rem];
+        const int n = 2 * K * IB_FIELDS, u0 = t - 64;
+        double a[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int u = u0 + k * (HPE_NT - 64);
+            const int vr = u >= K * IB_FIELDS ? 1 : 0;
+            a[k] = (u < n) ? src[vr * var_stride + (u - vr * K * IB_FIELDS)] : 0.0;
         }
-    }
-    if (t == 64) sm.dscal[4] = sw.pch[(size_t)(g - 1) * P + i];  // own pbest cost
-    if (t == 0) {
-        // end-of-generation update of g-1 (PSO.cpp:864-877) / initial gbest (:755-760)
-        const double fmin = bits_to_f64(sw.gmin[g - 1]);  // all-ones (no value) is a NaN
-        Sig s;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int u = u0 + k * (HPE_NT - 64);
+            if (u < n) (&ib[0][0][0])[(u >= K * IB_FIELDS ? IB_KMAX * IB_FIELDS - K * IB_FIELDS : 0) + u] = a[k];
+        }
+    } else {
+        // ---- wave 0, round 1: own state, draws, gbest bookkeeping, inbox tags / costs
+        if (t < HPE_DOF) {
+            xo = sw.xh[(size_t)(g - 1) * P * HPE_DOF + e];
+            vo = sw.v[e];
+            pbi = sw.pb[e];
+            rp = philox_u01(sw.seed, ST_RP, g, i, t);
+            rg = philox_u01(sw.seed, ST_RG, g, i, t);
+        }
+        const double pci = sw.pch[(size_t)(g - 1) * P + i];  // own pbest cost (uniform)
+        const double fmin = bits_to_f64(sw.gmin[g - 1]);     // all-ones (no value) is a NaN
+        const Sig pv = sw.sig[g > 1 ? g - 1 : 0];
+        double tg[2] = {0, 0}, tc[2] = {0, 0};
+        if (t < K) {
+#pragma unroll
+            for (int vr = 0; vr < 2; ++vr) {
+                const double *sl = sw.inbox + ib_index(sw, (g - 1) & 1, vr, i, t);
+                tg[vr] = sl[0];
+                tc[vr] = sl[1];
+            }
+        }
+        // end-of-generation update of g-1 (PSO.cpp:864-877) / initial gbest (:755-760),
+        // computed redundantly by every lane (uniform values)
+        Sig sg;
         if (g == 1) {
-            const bool imp = fmin < 1e100;
-            s.gcost = imp ? fmin : 1e100;
-            s.count = 100;  // PSO.cpp:768
-            s.topo = -1;
+            sg.gcost = fmin < 1e100 ? fmin : 1e100;
+            sg.count = 100;  // PSO.cpp:768
+            sg.topo = -1;
         } else {
-            const Sig pv = sw.sig[g - 1];
             const bool imp = fmin < pv.gcost;
-            s.gcost = imp ? fmin : pv.gcost;
-            s.count = imp ? 0 : pv.count + 1;
-            s.topo = pv.topo;
+            sg.gcost = imp ? fmin : pv.gcost;
+            sg.count = imp ? 0 : pv.count + 1;
+            sg.topo = pv.topo;
         }
-        if (s.count > 0) s.topo = g;  // topology rebuilt when count > 0 (PSO.cpp:790)
-        sm.iscal[0] = s.topo;
-        if (i == 0) sw.sig[g] = s;
-    }
-    __syncthreads();
-    sc.lap(0);
-    const int topo = sm.iscal[0], var = (topo == g) ? 1 : 0;
-    const double pci = sm.dscal[4];
-    // ---- informant = first argmin of pbest cost over {i} U incoming (PSO.cpp:810-812)
-    if (t >= 64 && t < 128) {
-        const int k = t - 64;
+        if (sg.count > 0) sg.topo = g;  // topology rebuilt when count > 0 (PSO.cpp:790)
+        if (i == 0 && t == 0) sw.sig[g] = sg;
+        if (t == 0) {
+            sm.iscal[0] = sg.topo;
+            sm.dscal[4] = pci;
+        }
+        const int topo = sg.topo;
+        var = (topo == g) ? 1 : 0;
+        sc.lap(0);
+        // informant = first argmin of pbest cost over {i} U incoming (PSO.cpp:810-812)
         double v = __builtin_inf();
         int idx = 0x7fffffff, slot = -1;
-        if (k < K) {
-            const long long tag = __double_as_longlong(ib[var][k][0]);
+        if (t < K) {
+            const long long tag = __double_as_longlong(var ? tg[1] : tg[0]);
             if ((tag >> 32) == (((long long)(g - 1) << 16) | topo)) {
-                v = ib[var][k][1];
+                v = var ? tc[1] : tc[0];
                 idx = (int)(tag & 0xffffffff);
-                slot = k;
+                slot = t;
             }
-        } else if (k == 63) {  // self (L = eye)
+        } else if (t == 63) {  // self (L = eye)
             v = pci;
             idx = i;
         }
         if (v != v) v = __builtin_inf();
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            const double ov = __shfl_xor(v, off);
-            const int oi = __shfl_xor(idx, off), os = __shfl_xor(slot, off);
-            if (ov < v || (ov == v && oi < idx)) {
-                v = ov;
-                idx = oi;
-                slot = os;
+        wave_argmin_lex(v, idx, slot, inf, islot);
+        sc.lap(1);
+    }
+    __syncthreads();  // informant rows in LDS
+    if (t < 64) {
+        // ---- velocity, position, check_constraints (PSO.cpp:824-842, 358-377)
+        if (t < HPE_DOF) {
+            const double *lb = sw.bounds, *ub = sw.bounds + HPE_DOF;
+            double vn;
+            if (inf == i) {
+                vn = W1 * vo + (C1 * rp) * (pbi - xo);
+            } else {
+                const double pbn = ib[var][islot][2 + t];
+                vn = (W1 * vo + (C1 * rp) * (pbi - xo)) + (C2 * rg) * (pbn - xo);
             }
+            double xn = xo + vn;
+            const double xr = xn;
+            if (xr < lb[t]) { xn = lb[t]; vn = 0.; }
+            if (xr > ub[t]) { xn = lb[t]; vn = 0.; }  // above max -> MIN (PSO.cpp:372)
+            sw.v[e] = vn;
+            sw.xh[(size_t)g * P * HPE_DOF + e] = xn;
+            sm.fk.th[t] = xn;
         }
-        if (k == 0) {
-            sm.iscal[1] = idx;
-            sm.iscal[2] = slot;
-        }
+        wave_sync();
+        sc.lap(2);
+        fk_wave(sm.fk, H);
     }
-    __syncthreads();
-    sc.lap(1);
-    const int inf = sm.iscal[1], islot = sm.iscal[2];
-    // ---- velocity, position, check_constraints (PSO.cpp:824-842, 358-377)
-    const double *lb = sw.bounds, *ub = sw.bounds + HPE_DOF;
-    if (t < HPE_DOF) {
-        double vn;
-        if (inf == i) {
-            vn = W1 * vo + (C1 * rp) * (pbi - xo);
-        } else {
-            const double pbn = ib[var][islot][2 + t];
-            vn = (W1 * vo + (C1 * rp) * (pbi - xo)) + (C2 * rg) * (pbn - xo);
-        }
-        double xn = xo + vn;
-        const double xr = xn;
-        if (xr < lb[t]) { xn = lb[t]; vn = 0.; }
-        if (xr > ub[t]) { xn = lb[t]; vn = 0.; }  // above max -> MIN (PSO.cpp:372)
-        sw.v[e] = vn;
-        sw.xh[(size_t)g * P * HPE_DOF + e] = xn;
-        sm.fk.th[t] = xn;
-    }
-    __syncthreads();
-    sc.lap(2);
+    __syncthreads();  // spheres, topology and own pbest cost published
+    const int topo = sm.iscal[0];
+    const double pci = sm.dscal[4];
+    if (q >= 3 * IB_FIELDS && q < 6 * IB_FIELDS) load_link(sw, g, i, q, topo, lr, ls);
     // ---- evaluation and pbest (PSO.cpp:848-861)
-    const double fx = eval_block<EV_COST, HPE_NT>(sm, o, cv, H, nullptr, pre);
+    const double fx = eval_block<EV_COST, HPE_NT, false>(sm, o, cv, H, nullptr, pre);
     sc.start();
     const bool better = fx < pci;
     const double pn = better ? fx : pci;
@@ -318,7 +347,7 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
         atomicMin(&sw.gmin[g], f64_to_bits(pn));
     }
     __syncthreads();
-    push_inbox(sw, g, i, topo, pn, sm.fk.th);
+    push_inbox(sw, g, i, q, lr, ls, q < 3 * IB_FIELDS ? g + 1 : topo, pn, sm.fk.th);
     sc.lap(3);
 }
 
@@ -326,37 +355,55 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
 // gbest / count sequence from gmin[], finds the last improving generation g* and takes
 // particles.col(first argmin pcost) of that generation; resets gmin[] for the next call.
 __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__restrict__ out) {
+    constexpr int CH = 2048;  // generations staged per pass
     __shared__ Smem sm;
+    __shared__ double gm[CH];
+    __shared__ int tp[CH];
     const int t = threadIdx.x, G = sw.G, P = sw.P;
+    double gcost = 1e100;
+    int last = -1, count = 100;
+    for (int base = 0; base <= G; base += CH) {
+        // all loads of the pass at once, then a serial replay from LDS by thread 0
+        for (int k = t; k < CH && base + k <= G; k += HPE_NT) {
+            gm[k] = bits_to_f64(sw.gmin[base + k]);  // all-ones (never written) is a NaN
+            tp[k] = (base + k >= 1) ? sw.sig[base + k].topo : -1;
+        }
+        __syncthreads();
+        if (t == 0) {
+            const int n = (G - base + 1) < CH ? (G - base + 1) : CH;
+            for (int k = 0; k < n; ++k) {
+                const int g = base + k;
+                const double fm = gm[k];
+                if (g == 0) {
+                    if (fm < gcost) {
+                        gcost = fm;
+                        last = 0;
+                    }
+                    continue;
+                }
+                if (fm < gcost) {
+                    gcost = fm;
+                    count = 0;
+                    last = g;
+                } else {
+                    count += 1;
+                }
+                if (sw.trace_g) {
+                    sw.trace_g[g - 1] = gcost;
+                    sw.trace_count[g - 1] = count;
+                    sw.trace_topo[g - 1] = tp[k];
+                }
+            }
+        }
+        __syncthreads();
+    }
     if (t == 0) {
-        double gcost = 1e100;
-        int last = -1, count = 100;
-        const double f0 = bits_to_f64(sw.gmin[0]);
-        if (f0 < gcost) {
-            gcost = f0;
-            last = 0;
-        }
-        for (int g = 1; g <= G; ++g) {
-            const double fm = bits_to_f64(sw.gmin[g]);
-            if (fm < gcost) {
-                gcost = fm;
-                count = 0;
-                last = g;
-            } else {
-                count += 1;
-            }
-            if (sw.trace_g) {
-                sw.trace_g[g - 1] = gcost;
-                sw.trace_count[g - 1] = count;
-                sw.trace_topo[g - 1] = sw.sig[g].topo;
-            }
-        }
         sm.iscal[2] = last;
         sm.dscal[5] = gcost;
     }
     __syncthreads();
-    const int last = sm.iscal[2];
-    const double gcost = sm.dscal[5];
+    last = sm.iscal[2];
+    gcost = sm.dscal[5];
     if (last >= 0) {
         const double *pc = sw.pch + (size_t)last * P;
         VI mine = {__builtin_inf(), 0};
