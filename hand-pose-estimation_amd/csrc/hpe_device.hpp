@@ -28,7 +28,23 @@
 #endif
 __device__ unsigned long long hpe_stamps[64];
 struct StampClock {
-    unsigned long long t;
+    unsigned long long t, t0 = 0, r0 = 0;
+    // whole-kernel span of block 0: shader cycles into slot k, 100 MHz ticks into k + 1
+    __device__ __forceinline__ void begin() {
+        if (HPE_STAMPS && blockIdx.x == 0 && threadIdx.x == 0) {
+            t0 = __builtin_amdgcn_s_memtime();
+            r0 = __builtin_amdgcn_s_memrealtime();
+            t = t0;
+        }
+    }
+    __device__ __forceinline__ void span(int k) {
+        if (HPE_STAMPS && blockIdx.x == 0 && threadIdx.x == 0) {
+            hpe_stamps[k] += __builtin_amdgcn_s_memtime() - t0;
+            hpe_stamps[k + 1] += __builtin_amdgcn_s_memrealtime() - r0;
+            hpe_stamps[32 + k] += 1;
+            hpe_stamps[32 + k + 1] += 1;
+        }
+    }
     __device__ __forceinline__ void start() {
         if (HPE_STAMPS && blockIdx.x == 0 && threadIdx.x == 0) t = __builtin_amdgcn_s_memtime();
     }
@@ -58,6 +74,7 @@ struct __align__(16) Smem {
     double red[16][4];
     double dscal[8];
     int iscal[16];
+    double draws[2 * HPE_DOF];  // rp, rg of the generation (k_pso_gen)
 };
 
 // Cloud + correspondences, either in LDS (staged) or in HBM.
@@ -245,10 +262,22 @@ __device__ __forceinline__ void wave_sum3(double &a, double &b, double &c) {
     c = ((readlane_f64(c, 0) + readlane_f64(c, 16)) + readlane_f64(c, 32)) + readlane_f64(c, 48);
 }
 
+__device__ __forceinline__ void wave_sum2(double &a, double &b) {
+    a += dpp_f64<0xB1>(a); b += dpp_f64<0xB1>(b);
+    a += dpp_f64<0x4E>(a); b += dpp_f64<0x4E>(b);
+    a += dpp_f64<0x141>(a); b += dpp_f64<0x141>(b);
+    a += dpp_f64<0x140>(a); b += dpp_f64<0x140>(b);
+    a = ((readlane_f64(a, 0) + readlane_f64(a, 16)) + readlane_f64(a, 32)) + readlane_f64(a, 48);
+    b = ((readlane_f64(b, 0) + readlane_f64(b, 16)) + readlane_f64(b, 32)) + readlane_f64(b, 48);
+}
+
 // Sum three per-thread doubles over NT threads in a fixed order; result in every thread.
-template <int NT>
+// REUSE = false: the caller never touches `red` again in this kernel, so the trailing
+// barrier that protects it is skipped.  c is not reduced when TWO (it stays 0).
+template <int NT, bool REUSE = true, bool TWO = false>
 __device__ __forceinline__ void block_sum3(double (*red)[4], double &a, double &b, double &c) {
-    wave_sum3(a, b, c);
+    if (TWO) wave_sum2(a, b);
+    else wave_sum3(a, b, c);
     const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
         red[w][0] = a;
@@ -265,8 +294,8 @@ __device__ __forceinline__ void block_sum3(double (*red)[4], double &a, double &
     }
     a = ra;
     b = rb;
-    c = rc;
-    __syncthreads();
+    c = TWO ? 0.0 : rc;
+    if (REUSE) __syncthreads();
 }
 
 // ---------------------------------------------------------------- cost terms
@@ -343,16 +372,19 @@ __device__ __forceinline__ Pt load_pt(const CloudView &cv, int it) {
 }
 // pre: the point of item threadIdx.x, loaded early by the caller (load_pt) so its
 // latency hides under FK.
+// gt: this thread's index among the NT threads searching for the particle.
 template <int NT, bool STORE_MATCH>
 __device__ __forceinline__ double search_align(const FkSm &f, const CloudView &cv,
                                                const DevHand *__restrict__ H,
-                                               int32_t *__restrict__ match, Pt pre) {
+                                               int32_t *__restrict__ match, Pt pre,
+                                               int gt = -1) {
+    if (gt < 0) gt = threadIdx.x;
     double acc = 0.0;
-    const int h = threadIdx.x & 1;
+    const int h = gt & 1;
     const float4 *Sf = f.Sf + 24 * h;
-    for (int it = threadIdx.x; it < 2 * cv.n; it += NT) {
+    for (int it = gt; it < 2 * cv.n; it += NT) {
         const int p = it >> 1;
-        const Pt q = (it == (int)threadIdx.x) ? pre : load_pt(cv, it);
+        const Pt q = (it == gt) ? pre : load_pt(cv, it);
         const double X = q.x, Y = q.y, Z = q.z;
         const float qx = (float)X, qy = (float)Y, qz = (float)Z;
         float d2[24];
@@ -428,6 +460,20 @@ __device__ __forceinline__ double align_frozen(const FkSm &f, const CloudView &c
 
 enum EvalMode { EV_COST = 0, EV_COST2_CORR = 1, EV_COST2_FROZEN = 2, EV_COST_STORE = 3 };
 
+// cal_cost of the particle in f.th by ONE wave (FK + search over 64 lanes): the
+// throughput form used when there are many more particles than CUs.  All lanes return
+// the total; pre = load_pt(cv, lane).
+__device__ __forceinline__ double eval_wave_cost(FkSm &f, const DevObs &o, const CloudView &cv,
+                                                 const DevHand *__restrict__ H, Pt pre) {
+    const int l = threadIdx.x & 63;
+    fk_wave(f, H);
+    double dep = (l < HPE_NS) ? depth_term(f, l, o, H) : 0.0;
+    double al = search_align<64, false>(f, cv, H, nullptr, pre, l);
+    double co = 0.0;
+    wave_sum3(al, dep, co);
+    return al * o.lambda + dep;
+}
+
 __device__ __forceinline__ CloudView obs_cloud(const DevObs &o) {
     return CloudView{o.cx, o.cy, o.cz, o.n};
 }
@@ -458,7 +504,7 @@ __device__ __forceinline__ double eval_block(Smem &sm, const DevObs &o, const Cl
     const bool coll = (MODE == EV_COST2_CORR || MODE == EV_COST2_FROZEN);
     double co = (coll && t < 144) ? collide_term(sm.fk, t, H) : 0.0;
     sc.lap(11);
-    block_sum3<NT>(sm.red, al, dep, co);
+    block_sum3<NT, false, !(MODE == EV_COST2_CORR || MODE == EV_COST2_FROZEN)>(sm.red, al, dep, co);
     sc.lap(12);
     const double align = al * o.lambda;
     if (t == 0) {

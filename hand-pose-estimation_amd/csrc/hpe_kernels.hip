@@ -210,14 +210,15 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_init(DevSwarm sw, const double *
 __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *__restrict__ og,
                                                     const DevHand *__restrict__ Hg, int g,
                                                     double W1, double C1, double C2) {
+    StampClock sc;
+    sc.begin();
     const DevObs o = *og;  // the selected frame (device-resident: graph-stable args)
     __shared__ Smem sm;
     __shared__ double ib[2][IB_KMAX][IB_FIELDS];
     const int i = blockIdx.x, t = threadIdx.x, P = sw.P, K = sw.K;
     stage_hand<HPE_NT>(sm.hand, Hg);
     const DevHand *__restrict__ H = &sm.hand;
-    StampClock sc;
-    sc.start();
+    sc.lap(4);
     const CloudView cv = obs_cloud(o);
     const Pt pre = load_pt(cv, t);  // this thread's first cloud point, used after FK
     const size_t e = (size_t)i * HPE_DOF + t;
@@ -226,6 +227,10 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
     if (q >= 0 && q < 3 * IB_FIELDS) load_link(sw, g, i, q, g + 1, lr, ls);
     double pbi = 0, xo = 0, vo = 0, rp = 0, rg = 0;  // own state (lanes t < 26 of wave 0)
     int inf = 0, islot = -1, var = 0;
+    if (t >= 64 && t < 64 + 2 * HPE_DOF) {  // wave 1 draws rp, rg while wave 0 waits on loads
+        const int j = t - 64, d = j < HPE_DOF ? j : j - HPE_DOF;
+        sm.draws[j] = philox_u01(sw.seed, j < HPE_DOF ? ST_RP : ST_RG, g, i, d);
+    }
     if (t >= 64) {
         // ---- waves 1..7: both informant inboxes (payload rows) into LDS, loads first
         const double *src = sw.inbox + ib_index(sw, (g - 1) & 1, 0, i, 0);
@@ -249,8 +254,6 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
             xo = sw.xh[(size_t)(g - 1) * P * HPE_DOF + e];
             vo = sw.v[e];
             pbi = sw.pb[e];
-            rp = philox_u01(sw.seed, ST_RP, g, i, t);
-            rg = philox_u01(sw.seed, ST_RG, g, i, t);
         }
         const double pci = sw.pch[(size_t)(g - 1) * P + i];  // own pbest cost (uniform)
         const double fmin = bits_to_f64(sw.gmin[g - 1]);     // all-ones (no value) is a NaN
@@ -304,10 +307,12 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
         wave_argmin_lex(v, idx, slot, inf, islot);
         sc.lap(1);
     }
-    __syncthreads();  // informant rows in LDS
+    __syncthreads();  // informant rows and draws in LDS
     if (t < 64) {
         // ---- velocity, position, check_constraints (PSO.cpp:824-842, 358-377)
         if (t < HPE_DOF) {
+            rp = sm.draws[t];
+            rg = sm.draws[HPE_DOF + t];
             const double *lb = sw.bounds, *ub = sw.bounds + HPE_DOF;
             double vn;
             if (inf == i) {
@@ -349,6 +354,184 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
     __syncthreads();
     push_inbox(sw, g, i, q, lr, ls, q < 3 * IB_FIELDS ? g + 1 : topo, pn, sm.fk.th);
     sc.lap(3);
+    sc.span(5);
+}
+
+// ---------------------------------------------------------------- wave-per-particle form
+// For swarms much larger than the CU count (BASELINE configs 4 and 5) one workgroup per
+// particle leaves the SIMDs idle during the single-wave FK and reductions; here each wave
+// carries one particle end to end (same arithmetic and draws, per-wave syncs only) and
+// PW_WPB particles share a workgroup, so the CU interleaves many particles' latency
+// chains.  The informant's pbest row is read from the inbox after the choice.
+#define PW_WPB 4
+#define PW_NT (64 * PW_WPB)
+
+__device__ __forceinline__ void push_lane_links(const DevSwarm &sw, int g, int i, int l, int tt0,
+                                                int tt1, int (&lr)[3], int (&ls)[3]) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int q = l + 64 * k;
+        const int tt = (q < 3 * IB_FIELDS) ? tt0 : tt1;
+        load_link(sw, g, i, q, tt, lr[k], ls[k]);
+    }
+}
+
+__global__ __launch_bounds__(PW_NT) void k_pso_init_w(DevSwarm sw, const double *__restrict__ x0,
+                                                      const DevObs *__restrict__ og,
+                                                      const DevHand *__restrict__ Hg) {
+    const DevObs o = *og;
+    __shared__ DevHand hs;
+    __shared__ FkSm fks[PW_WPB];
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    const int i = blockIdx.x * PW_WPB + w, P = sw.P;
+    const bool valid = i < P;
+    const int ic = valid ? i : P - 1;
+    stage_hand<PW_NT>(hs, Hg);
+    const DevHand *__restrict__ H = &hs;
+    FkSm &f = fks[w];
+    int lr[3], ls[3];
+    push_lane_links(sw, 0, ic, l, 1, -1, lr, ls);
+    const CloudView cv = obs_cloud(o);
+    const Pt pre = load_pt(cv, l);
+    const double *sd = sw.bounds + 2 * HPE_DOF;
+    if (l < HPE_DOF) {  // particles = x0 + randn % std (PSO.cpp:67-72)
+        const size_t e = (size_t)ic * HPE_DOF + l;
+        const double x = x0[l] + sw.normals[e] * sd[l];
+        f.th[l] = x;
+        if (valid) {
+            sw.xh[e] = x;
+            sw.pb[e] = x;
+            sw.v[e] = 0.0;
+        }
+    }
+    __syncthreads();  // hand staged
+    const double c = eval_wave_cost(f, o, cv, H, pre);
+    if (!valid) return;
+    if (l == 0) {
+        sw.pch[i] = c;
+        atomicMin(&sw.gmin[0], f64_to_bits(c));
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) push_inbox(sw, 0, i, l + 64 * k, lr[k], ls[k], 1, c, f.th);
+}
+
+__global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *__restrict__ og,
+                                                     const DevHand *__restrict__ Hg, int g,
+                                                     double W1, double C1, double C2) {
+    const DevObs o = *og;
+    __shared__ DevHand hs;
+    __shared__ FkSm fks[PW_WPB];
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    const int i = blockIdx.x * PW_WPB + w, P = sw.P, K = sw.K;
+    const bool valid = i < P;
+    const int ic = valid ? i : P - 1;
+    stage_hand<PW_NT>(hs, Hg);
+    const DevHand *__restrict__ H = &hs;
+    FkSm &f = fks[w];
+    // ---- round 1: every load of the generation, all independent
+    int lr[3], ls[3];
+    push_lane_links(sw, g, ic, l, g + 1, -1, lr, ls);  // var-0 links after the decision
+    const CloudView cv = obs_cloud(o);
+    const Pt pre = load_pt(cv, l);
+    const size_t e = (size_t)ic * HPE_DOF + l;
+    double xo = 0, vo = 0, pbi = 0, rp = 0, rg = 0;
+    if (l < HPE_DOF) {
+        xo = sw.xh[(size_t)(g - 1) * P * HPE_DOF + e];
+        vo = sw.v[e];
+        pbi = sw.pb[e];
+        rp = philox_u01(sw.seed, ST_RP, g, ic, l);
+        rg = philox_u01(sw.seed, ST_RG, g, ic, l);
+    }
+    const double pci = sw.pch[(size_t)(g - 1) * P + ic];
+    const double fmin = bits_to_f64(sw.gmin[g - 1]);
+    const Sig pv = sw.sig[g > 1 ? g - 1 : 0];
+    double tg[2] = {0, 0}, tc[2] = {0, 0};
+    if (l < K) {
+#pragma unroll
+        for (int vr = 0; vr < 2; ++vr) {
+            const double *sl = sw.inbox + ib_index(sw, (g - 1) & 1, vr, ic, l);
+            tg[vr] = sl[0];
+            tc[vr] = sl[1];
+        }
+    }
+    // ---- end-of-generation update of g-1 (PSO.cpp:864-877), uniform
+    Sig sg;
+    if (g == 1) {
+        sg.gcost = fmin < 1e100 ? fmin : 1e100;
+        sg.count = 100;
+        sg.topo = -1;
+    } else {
+        const bool imp = fmin < pv.gcost;
+        sg.gcost = imp ? fmin : pv.gcost;
+        sg.count = imp ? 0 : pv.count + 1;
+        sg.topo = pv.topo;
+    }
+    if (sg.count > 0) sg.topo = g;
+    if (i == 0 && l == 0) sw.sig[g] = sg;
+    const int topo = sg.topo, var = (topo == g) ? 1 : 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int q = l + 64 * k;
+        if (q >= 3 * IB_FIELDS) load_link(sw, g, ic, q, topo, lr[k], ls[k]);
+    }
+    // ---- informant (PSO.cpp:810-812)
+    double v = __builtin_inf();
+    int idx = 0x7fffffff, slot = -1;
+    if (l < K) {
+        const long long tag = __double_as_longlong(var ? tg[1] : tg[0]);
+        if ((tag >> 32) == (((long long)(g - 1) << 16) | topo)) {
+            v = var ? tc[1] : tc[0];
+            idx = (int)(tag & 0xffffffff);
+            slot = l;
+        }
+    } else if (l == 63) {
+        v = pci;
+        idx = ic;
+    }
+    if (v != v) v = __builtin_inf();
+    int inf, islot;
+    wave_argmin_lex(v, idx, slot, inf, islot);
+    // ---- velocity, position, check_constraints (PSO.cpp:824-842, 358-377)
+    if (l < HPE_DOF) {
+        const double *lb = sw.bounds, *ub = sw.bounds + HPE_DOF;
+        double vn;
+        if (inf == ic) {
+            vn = W1 * vo + (C1 * rp) * (pbi - xo);
+        } else {
+            const double pbn = sw.inbox[ib_index(sw, (g - 1) & 1, var, ic, islot) + 2 + l];
+            vn = (W1 * vo + (C1 * rp) * (pbi - xo)) + (C2 * rg) * (pbn - xo);
+        }
+        double xn = xo + vn;
+        const double xr = xn;
+        if (xr < lb[l]) { xn = lb[l]; vn = 0.; }
+        if (xr > ub[l]) { xn = lb[l]; vn = 0.; }  // above max -> MIN (PSO.cpp:372)
+        if (valid) {
+            sw.v[e] = vn;
+            sw.xh[(size_t)g * P * HPE_DOF + e] = xn;
+        }
+        f.th[l] = xn;
+    }
+    __syncthreads();  // hand staged (the only block-wide sync)
+    // ---- evaluation and pbest (PSO.cpp:848-861)
+    const double fx = eval_wave_cost(f, o, cv, H, pre);
+    if (!valid) return;
+    const bool better = fx < pci;
+    const double pn = better ? fx : pci;
+    if (l < HPE_DOF) {
+        const double row = better ? f.th[l] : pbi;
+        sw.pb[e] = row;
+        f.th[l] = row;
+    }
+    if (l == 0) {
+        sw.pch[(size_t)g * P + i] = pn;
+        atomicMin(&sw.gmin[g], f64_to_bits(pn));
+    }
+    wave_sync();
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int q = l + 64 * k;
+        push_inbox(sw, g, i, q, lr[k], ls[k], q < 3 * IB_FIELDS ? g + 1 : topo, pn, f.th);
+    }
 }
 
 // Last end-of-generation update and bestp = gbest_pos (PSO.cpp:864-882).  Replays the

@@ -238,3 +238,28 @@ def test_edge_small_clouds(oracle, ora_hand, gpu_hand):
     cf = hpe.costfunc(gpu_hand, om)
     np.testing.assert_allclose(cf.cal_cost_batch(oracle_np.X0[None]),
                                oracle.eval_costs(ora_hand, obs, oracle_np.X0[None]), rtol=RTOL)
+
+
+@pytest.mark.parametrize("P,maxiter", [(32, 11), (7, 4), (1, 3), (1030, 3)])
+def test_pso_evolve_wave_form(oracle, ora_hand, np_hand, P, maxiter, monkeypatch):
+    """The one-wave-per-particle generation kernels (used for large swarms) against the
+    oracle, including a ragged last workgroup (P not a multiple of 4)."""
+    import hpe
+    monkeypatch.setenv("HPE_PSO_FORM", "wave")
+    gh = hpe.reference_hand(device=0)  # context created with the wave form forced
+    truth = hand_data.trajectory(2, seed=9)[1]
+    d = oracle_np.render_depth_mm(np_hand, truth)
+    obs, om = _obs_pair(oracle, gh, d)
+    cf = hpe.costfunc(gh, om)
+    ub, lb, sd = oracle_np.reference_bounds()
+    pso = hpe.PSO()
+    pso.set_pso_params(ub, lb, sd, 0.7298, 1.49618, 1.49618, maxiter, 1e-8, 1e-8)
+    bestp = np.zeros(26)
+    x0 = oracle_np.X0.copy()
+    assert pso.pso_evolve(cf, x0, P, bestp) == 1
+    rb, rc, tr = oracle.pso_evolve(ora_hand, obs, x0, P, maxiter, lb, ub, sd, seed=1000)
+    np.testing.assert_allclose(bestp, rb, rtol=0, atol=1e-6)
+    assert abs(pso.last_gbest_cost - rc) <= 1e-8 * abs(rc)
+    g, cnt, topo = pso.trace(cf)
+    np.testing.assert_allclose(g, tr["gbest"], rtol=1e-8)
+    assert np.array_equal(cnt, tr["count"]) and np.array_equal(topo, tr["topo"])

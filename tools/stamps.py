@@ -27,7 +27,8 @@ x = np.ascontiguousarray(poses[0])
 ctx.select_frame(0)
 lib.hpe_track_frame(ctx.h, P, 1, _lib.ptr(x, C.c_double), None)
 lib.hpe_debug_stamps(st.ctypes.data_as(C.POINTER(C.c_uint64)))  # reset
-names = {0: "gen: argmin+sig", 1: "gen: informant", 2: "gen: velocity", 3: "gen: pbest tail",
+names = {4: "gen: prologue (og + hand)", 5: "gen: block-0 span (cycles)",
+         6: "gen: block-0 span (100MHz ticks)", 0: "gen: argmin+sig", 1: "gen: informant", 2: "gen: velocity", 3: "gen: pbest tail",
          10: "eval: fk", 11: "eval: search/align+depth+coll", 12: "eval: block_sum",
          13: "fk: trig phase", 14: "fk: chain+spheres phase", 15: "wave: depth issue",
          16: "wave: align frozen", 17: "wave: collision", 18: "wave: 3 reductions",
