@@ -6,3 +6,4 @@ mkdir -p $O
 timeout -k 10 400 python -m pytest tests -x -q -m gpu > $O/pytest_gpu.log 2>&1 && \
 timeout -k 10 200 python tools/stamps.py 4 > $O/stamps.log 2>&1 && \
 timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench.log 2>&1
+timeout -k 10 60 ./tools/ubench > $O/ubench.log 2>&1
