@@ -840,4 +840,5 @@ extern "C" int hpe_debug_stamps(unsigned long long *out64) {
     return HPE_STAMPS;
 }
 
+#include "hpe_prep.hpp"
 #include "hpe_api.inc"

@@ -90,6 +90,22 @@ class Context:
     def select_frame(self, slot):
         self.check(self.lib.hpe_select_frame(self._h, slot))
 
+    def prepare_frame(self, slot, depth_mm, to_cm=True, downsample=True, focal=241.42):
+        """observedmodel::next_frame on the GPU into `slot` (asynchronous)."""
+        d = np.ascontiguousarray(depth_mm, dtype=np.float32).reshape(IMG_H, IMG_W)
+        self.check(self.lib.hpe_prepare_frame(self._h, slot, ptr(d, C.c_float), int(to_cm),
+                                              int(downsample), float(focal)))
+
+    def frame_readback(self, slot):
+        depth = np.zeros((IMG_H, IMG_W)); dt = np.zeros((IMG_H, IMG_W), dtype=np.float32)
+        cloud = np.zeros((IMG_H * IMG_W, 3)); n = C.c_int32(0)
+        scale = C.c_double(0); dtmax = C.c_double(0)
+        self.check(self.lib.hpe_frame_readback(self._h, slot, ptr(depth, C.c_double),
+                                               ptr(dt, C.c_float), ptr(cloud, C.c_double),
+                                               C.byref(n), C.byref(scale), C.byref(dtmax)))
+        return dict(depth_cm=depth, dt=dt, cloud=cloud[:n.value].copy(), scale=scale.value,
+                    dtmax=dtmax.value)
+
     def render_depth(self, theta, focal=241.42):
         th = _lib.as_f64(theta, (26,))
         out = np.zeros((IMG_H, IMG_W), dtype=np.float32)

@@ -47,6 +47,8 @@ SIGNATURES = {
     "hpe_store_frame": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(Frame)]),
     "hpe_select_frame": (C.c_int, [C.c_void_p, C.c_int]),
     "hpe_set_frame": (C.c_int, [C.c_void_p, C.POINTER(Frame)]),
+    "hpe_prepare_frame": (C.c_int, [C.c_void_p, C.c_int, fp, C.c_int, C.c_int, C.c_double]),
+    "hpe_frame_readback": (C.c_int, [C.c_void_p, C.c_int, dp, fp, dp, ip, dp, dp]),
     "hpe_build_spheres": (C.c_int, [C.c_void_p, dp, C.c_int, dp, dp]),
     "hpe_eval_costs": (C.c_int, [C.c_void_p, dp, C.c_int, C.c_int, dp, ip]),
     "hpe_cal_cost2": (C.c_int, [C.c_void_p, dp, ip, C.c_int, dp, dp]),

@@ -92,6 +92,22 @@ int hpe_store_frame(hpe_ctx *ctx, int slot, const hpe_frame *frame);
 int hpe_select_frame(hpe_ctx *ctx, int slot);
 int hpe_set_frame(hpe_ctx *ctx, const hpe_frame *frame);
 
+/* observedmodel::next_frame on the GPU (observedmodel.cpp:110-219, 272-369): the raw
+ * depth .bin (float mm, 240x320 row-major, host memory) is copied through a pinned
+ * buffer and preprocessed by one workgroup on the context's preprocessing stream --
+ * depth cm, cloud (down-sampled to 250 points when `downsample`), cm-per-pixel scale,
+ * 5x5 chamfer distance transform and its max -- straight into frame slot `slot`.
+ * Asynchronous: the call returns once the host buffer is copied; hpe_select_frame(slot)
+ * orders the tracking stream after it, so frame f+1 is prepared while frame f is tracked.
+ * Cloud, depth, DT, its max and the scale equal hpe_preprocess_depth bit for bit. */
+int hpe_prepare_frame(hpe_ctx *ctx, int slot, const float *depth_mm, int to_cm, int downsample,
+                      double focal);
+
+/* Copies a stored or prepared frame back to the host (tests, debugging); synchronises.
+ * cloud: n*3 doubles (capacity 76800*3); any output may be NULL. */
+int hpe_frame_readback(hpe_ctx *ctx, int slot, double *depth_cm, float *dt, double *cloud,
+                       int32_t *n_out, double *scale_out, double *dtmax_out);
+
 /* handmodel::build_hand_model for a batch (handmodel.cpp:259-298).
  * theta: 26*P; S_out: P*48*3; joints_out (optional, may be NULL): P*21*3
  * (hand_joints, handmodel.cpp:291-296). */

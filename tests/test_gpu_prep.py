@@ -1,0 +1,83 @@
+"""GPU preprocessing (hpe_prepare_frame) against the host preprocessing
+(hpe_preprocess_depth, itself bit-exact against the C oracle: tests/test_host.py).
+
+Depth, cloud, distance transform, its max, the cloud size and the cm-per-pixel scale
+(Armadillo's two-accumulator mean replayed in order) must be identical.
+Edge cases as observedmodel has them: empty frame (250 zero points when down-sampling,
+NaN scale), a single pixel, a full frame, frames touching the image border."""
+import numpy as np
+import pytest
+
+import hand_data
+import oracle_np
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gh():
+    import hpe
+    return hpe.reference_hand(device=0)
+
+
+def _frames(np_hand):
+    out = []
+    for seed in (0, 3):
+        for th in hand_data.trajectory(3, seed=seed):
+            out.append(oracle_np.render_depth_mm(np_hand, th))
+    e = np.zeros((240, 320), np.float32)
+    one = e.copy(); one[100, 200] = 300.0
+    full = np.full((240, 320), 455.5, np.float32)
+    edge = e.copy(); edge[0:6, 0:9] = 250.0; edge[-4:, -7:] = 251.0; edge[120, :] = 260.0
+    rng = np.random.default_rng(1)
+    speck = np.where(rng.random((240, 320)) < 0.02, rng.uniform(200, 600, (240, 320)), 0).astype(np.float32)
+    return out + [e, one, full, edge, speck]
+
+
+def _check(a, b):
+    np.testing.assert_array_equal(a["depth_cm"], b["depth_cm"])
+    np.testing.assert_array_equal(a["dt"], b["dt"])
+    np.testing.assert_array_equal(a["cloud"], b["cloud"])
+    assert a["dtmax"] == b["dtmax"]
+    if np.isnan(b["scale"]):
+        assert np.isnan(a["scale"])
+    else:
+        assert a["scale"] == b["scale"]
+
+
+@pytest.mark.parametrize("downsample", [True, False])
+def test_prepare_matches_host(gh, np_hand, downsample):
+    import hpe
+    for k, d in enumerate(_frames(np_hand)):
+        gh.ctx.prepare_frame(100 + k, d, downsample=downsample)
+    for k, d in enumerate(_frames(np_hand)):
+        _check(gh.ctx.frame_readback(100 + k), hpe.preprocess_depth(d, downsample=downsample))
+
+
+def test_prepared_frames_track_like_oracle(gh, oracle, ora_hand, np_hand):
+    """test_full's loop on device-prepared frames (prepared one frame ahead)."""
+    import hpe
+    poses = hand_data.trajectory(3, seed=12)
+    depth = [oracle_np.render_depth_mm(np_hand, th) for th in poses]
+    ub, lb, sd = oracle_np.reference_bounds()
+    pso = hpe.PSO()
+    pso.set_pso_params(ub, lb, sd, 0.7298, 1.49618, 1.49618, 6, 1e-8, 1e-8)
+    pso._push(gh.ctx)
+    x_gpu = oracle_np.X0.copy(); x_ref = oracle_np.X0.copy()
+    gh.ctx.prepare_frame(200, depth[0])
+    import ctypes as C
+    from hpe._lib import ptr
+    for f in range(3):
+        if f + 1 < 3:
+            gh.ctx.prepare_frame(200 + f + 1, depth[f + 1])
+        gh.ctx.select_frame(200 + f)
+        gh.ctx.frame_token = None
+        cost = C.c_double(0)
+        gh.ctx.check(gh.ctx.lib.hpe_track_frame(gh.ctx.h, 32, 1, ptr(x_gpu, C.c_double),
+                                                C.byref(cost)))
+        obs = oracle.preprocess(depth[f])
+        x_ref, _ = oracle.refine(ora_hand, obs, x_ref)
+        x_ref, _, _ = oracle.pso_evolve(ora_hand, obs, x_ref, 32, 6, lb, ub, sd)
+        cr = oracle.cal_cost(ora_hand, obs, x_ref)
+        np.testing.assert_allclose(x_gpu, x_ref, rtol=0, atol=1e-6)
+        assert abs(cost.value - cr) <= 1e-8 * abs(cr)
