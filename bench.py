@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--generations", type=int, default=30)
     ap.add_argument("--full-cloud", action="store_true", help="no down-sampling (N ~ 9.3k)")
     ap.add_argument("--no-refine", action="store_true")
+    ap.add_argument("--resident", action="store_true",
+                    help="preprocess every frame before timing (default: each step prepares "
+                         "the next frame from host depth on the GPU, overlapped)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--seed", type=int, default=0, help="trajectory seed")
@@ -80,12 +83,12 @@ def cpu_baseline(args, sizes_hint):
     P, G = args.particles, args.generations
     ub, lb, sd = hpe.reference_bounds()
     poses = synth.trajectory(64, args.seed)
-    frames = [o.preprocess(oracle_np.render_depth_mm(nh, poses[f]),
-                           downsample=not args.full_cloud) for f in range(min(len(poses), 64))]
+    raw = [oracle_np.render_depth_mm(nh, poses[f]) for f in range(len(poses))]
     x = poses[0].copy()
-    done, t0 = 0, time.perf_counter()
+    done, t0, n_pts = 0, time.perf_counter(), 0
     while True:
-        obs = frames[done % len(frames)]
+        obs = o.preprocess(raw[done % len(raw)], downsample=not args.full_cloud)  # next_frame
+        n_pts = obs.n
         if not args.no_refine:
             x, _ = o.refine(h, obs, x)
         x, _, _ = o.pso_evolve(h, obs, x, P, G + 1, lb, ub, sd, seed=1000, nthreads=threads)
@@ -96,7 +99,7 @@ def cpu_baseline(args, sizes_hint):
             break
     return {"value": P * (G + 1) * done / el, "unit": "particle-evals/s", "cores": threads,
             "kind": "port", "tracked_fps": done / el,
-            "sample": f"{done} tracked frames ({P}p x {G} gen, N={frames[0].n}, "
+            "sample": f"{done} tracked frames incl. preprocessing ({P}p x {G} gen, N={n_pts}, "
                       f"refine={'off' if args.no_refine else 'on'}) of the same synthetic "
                       f"sequence in {el:.1f} s, oracle/hpe_oracle.c with {threads} OpenMP threads"}
 
@@ -138,8 +141,18 @@ def main():
     hand = hpe.reference_hand(device=local)
     ctx, lib = hand.ctx, hand.ctx.lib
     n_frames = args.warmup + args.steps
-    poses, sizes = synth.load_sequence(ctx, n_frames, seed=args.seed,
-                                       downsample=not args.full_cloud)
+    ds = not args.full_cloud
+    # the input: raw 240x320 float32 mm depth frames in host memory, as load_data reads
+    # them from .bin files (synthetic: rendered once from a seeded pose trajectory)
+    poses = synth.trajectory(n_frames, args.seed)
+    raw = [np.ascontiguousarray(ctx.render_depth(th)) for th in poses]
+    sizes = [len(hpe.preprocess_depth(d, True, ds)["cloud"]) for d in raw]
+    NSLOT = 4  # frame slots in rotation: frame f+1 is prepared while frame f is tracked
+    slot = (lambda f: f) if args.resident else (lambda f: f % NSLOT)
+    if args.resident:  # frames preprocessed and resident in HBM before the timed region
+        for f in range(n_frames):
+            ctx.prepare_frame(slot(f), raw[f], True, ds)
+        ctx.check(lib.hpe_sync(ctx.h))
     ub, lb, sd = hpe.reference_bounds()
     ctx.check(lib.hpe_set_pso_params(ctx.h, hpe._lib.ptr(ub, C.c_double),
                                      hpe._lib.ptr(lb, C.c_double), hpe._lib.ptr(sd, C.c_double),
@@ -153,12 +166,17 @@ def main():
     refine = 0 if args.no_refine else 1
 
     def step(f):
-        ctx.select_frame(f)
-        ctx.check(lib.hpe_track_frame_dev(ctx.h, P, refine, C.c_void_p(state.data_ptr())))
+        if args.resident:
+            ctx.select_frame(slot(f))
+            ctx.check(lib.hpe_track_frame_dev(ctx.h, P, refine, C.c_void_p(state.data_ptr())))
+        else:  # frame f tracked while frame f+1 is prepared inside its refine launch
+            ctx.track_pipelined(P, refine, state.data_ptr(), raw[f + 1] if f + 1 < n_frames else None)
         if world > 1:  # best-of-N exchange on the tracker's own stream (no host sync)
             with torch.cuda.stream(ext):
                 exchange_best(state, gathered)
 
+    if not args.resident:
+        ctx.pipeline_begin(raw[0], True, ds)
     for f in range(args.warmup):
         step(f)
     ctx.check(lib.hpe_sync(ctx.h))
@@ -170,10 +188,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    host_s = 0.0
     for k, f in enumerate(range(args.warmup, n_frames)):
+        h0 = time.perf_counter()
         ev[k][0].record(ext)
         step(f)
         ev[k][1].record(ext)
+        host_s += time.perf_counter() - h0
     ctx.check(lib.hpe_sync(ctx.h))
     torch.cuda.synchronize()
     if world > 1:
@@ -188,11 +209,14 @@ def main():
     # per-kernel durations: the same frames once more with every dispatch bracketed by
     # hipExtLaunchKernel start/stop events (direct launches; kernels are identical)
     ctx.check(lib.hpe_profile_enable(ctx.h, 1))
+    if not args.resident:
+        ctx.pipeline_begin(raw[args.warmup], True, ds)
     for f in range(args.warmup, n_frames):
         step(f)
     ctx.check(lib.hpe_sync(ctx.h))
     prof = {}
-    for name, kid in (("k_pso_gen", 0), ("k_refine", 1), ("k_pso_init", 2), ("k_pso_final", 3)):
+    for name, kid in (("k_pso_gen", 0), ("k_refine", 1), ("k_pso_init", 2), ("k_pso_final", 3),
+                      ("k_preprocess", 4)):
         nl = C.c_int32(0); tot = C.c_double(0); mn = C.c_double(0); mx = C.c_double(0)
         ctx.check(lib.hpe_profile_read_kernel(ctx.h, kid, C.byref(nl), C.byref(tot),
                                               C.byref(mn), C.byref(mx)))
@@ -230,7 +254,9 @@ def main():
         "dtype": "f32+f64",
         "data": "synthetic: seeded 26-DOF trajectory rendered from the 48-sphere model "
                 "into 240x320 float32 mm depth (no MSRA Subject1 on the box)",
-        "config": {"workload": "tracked frame = refine_init_pose + pso_evolve + cal_cost(bestp)",
+        "config": {"workload": ("tracked frame = " + ("" if args.resident else
+                                "next_frame preprocessing (GPU, fused into the refine launch) + ") +
+                                "refine_init_pose + pso_evolve + cal_cost(bestp)"),
                    "particles": P, "generations": G, "maxiter": G + 1,
                    "cloud_points": n_pts, "refine": bool(refine),
                    "parallelism": f"subswarms x{world}, all-gather best per frame"},
@@ -251,6 +277,7 @@ def main():
                     "latency-bound (one particle per workgroup, 31 dependent launches per "
                     "frame), DESIGN.md §5"},
         "kernels": prof,
+        "host_us_per_step": host_s / args.steps * 1e6,
     }
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args, sizes)

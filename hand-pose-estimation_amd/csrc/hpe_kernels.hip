@@ -13,6 +13,7 @@
 // One workgroup of HPE_NT threads per particle; see hpe_device.hpp for the block-level
 // pieces and DESIGN.md for layout, rooflines and the parity argument.
 #include "hpe_device.hpp"
+#include "hpe_prep.hpp"
 #include "../../include/hpe.h"
 
 // ------------------------------------------------------------------ batch kernels
@@ -645,13 +646,29 @@ __device__ __forceinline__ void gold_down(double a, double &b, double &alpha) {
     alpha = 0.5 * (a + alpha);
 }
 
+// Grid 1 or 1 + PREP_WG: workgroup 0 refines the selected frame (do_refine != 0); the
+// others, when present, prepare the NEXT frame meanwhile (hpe_prep.hpp) on
+// CUs this single-workgroup refine leaves idle -- one launch, one stream, no cross-queue
+// dependencies in the frame loop.
 template <bool STAGED>
 __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, const DevObs *__restrict__ og,
                                                   const DevHand *__restrict__ Hg,
                                                   int32_t *__restrict__ match_g,
-                                                  int *__restrict__ evals_out) {
+                                                  int *__restrict__ evals_out, int do_refine,
+                                                  PrepArgs pa) {
+    extern __shared__ __align__(16) unsigned char dyn[];  // staged cloud + matchId / prep
+    if (blockIdx.x >= 1) {
+        const unsigned long long t0 = HPE_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+        prep_workgroup(pa, blockIdx.x - 1, dyn);
+        if (HPE_STAMPS && threadIdx.x == 0) {  // diagnostic build: prep workgroup spans
+            const int k = (blockIdx.x - 1 < PREP_BANDS) ? 24 : 25;
+            atomicAdd(&hpe_stamps[k], __builtin_amdgcn_s_memtime() - t0);
+            atomicAdd(&hpe_stamps[32 + k], 1ull);
+        }
+        return;
+    }
+    if (!do_refine) return;
     const DevObs o = *og;  // the selected frame (device-resident: graph-stable args)
-    extern __shared__ __align__(16) unsigned char dyn[];  // staged cloud + matchId
     __shared__ RefineSm rs;
     __shared__ DevHand hs;  // hand constants in LDS: keeps them out of the loop's registers
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
@@ -840,5 +857,4 @@ extern "C" int hpe_debug_stamps(unsigned long long *out64) {
     return HPE_STAMPS;
 }
 
-#include "hpe_prep.hpp"
 #include "hpe_api.inc"

@@ -1,21 +1,32 @@
-// hpe_prep.hpp -- observedmodel preprocessing on the GPU, one
-// workgroup per frame, so a frame is prepared on a side stream while the previous one is
-// tracked:
+// hpe_prep.hpp -- observedmodel preprocessing on the GPU:
 //   depth mm -> cm                                   (observedmodel.cpp:296-308)
 //   point cloud of the non-zero pixels, row-major    (observedmodel.cpp:110-169)
 //   cm-per-pixel scale = mean of 2 / |d(u,v)|        (observedmodel.cpp:171-202)
 //   down-sample to rows k * floor(N / 250)           (observedmodel.cpp:204-217)
 //   5x5 chamfer distance transform of the background (observedmodel.cpp:313-358,
 //     OpenCV distanceTransform(CV_DIST_L2, 5): 16.16 fixed point, weights 1 / 1.4 / 2.1969)
-// The DT is integer min-plus arithmetic, so the row scans (T_c = min(a_c, T_{c-1} + 1))
-// computed as block prefix minima give exactly the raster-scan values.  The cloud and
-// depth are the host's arithmetic (-ffp-contract=off) and the scale mean is summed in
-// Armadillo's order (two alternating sequential accumulators): bit-identical results.
+//
+// Workgroups (PREP_WG of them, PREP_NT threads each, in one launch):
+//   PREP_BANDS "band" workgroups: 30 image rows each -- depth, per-pixel cloud point and
+//     scale term, compacted in pixel order within the band.  The last band to finish
+//     merges: band offsets, the scale mean replayed in Armadillo's order (two alternating
+//     sequential accumulators), the (down-sampled) cloud.
+//   one DT workgroup: the chamfer raster scans by ONE wave, lane l holding columns
+//     5l..5l+4, rows in registers; the in-row dependency T_c = min(a_c, T_{c-1} + 1) is a
+//     prefix minimum (lane-serial over 5 columns, DPP across lanes).  Integer min-plus
+//     arithmetic: exactly the raster-scan values.
+// Results equal hpe_preprocess_depth bit for bit.  Hand-offs between workgroups follow
+// MI355X_MICROARCH.md (inter-workgroup visibility): every storing wave waits for its
+// stores, workgroup barrier, agent release, arrival counter; the last arriver acquires.
 #pragma once
 #include "hpe_device.hpp"
 
-#define PREP_NT 1024
-#define PREP_CH 4096  // scale terms staged in LDS per pass
+#define PREP_NT 512
+#define PREP_BANDS 8
+#define PREP_WG (PREP_BANDS + 1)
+#define PREP_ROWS (HPE_IMG_H / PREP_BANDS)      // 30
+#define PREP_BAND_PIX (PREP_ROWS * HPE_IMG_W)  // 9600
+#define PREP_CH 4096                           // scale terms staged in LDS per pass
 #define DT_HV 65536
 #define DT_DIAG 91750
 #define DT_LONG 143976
@@ -24,7 +35,26 @@
 struct PrepInfo {
     int n_full, n;
     double scale, dtmax;
+    int band_n[PREP_BANDS], band_h[PREP_BANDS];  // points / scale terms per band
 };
+
+// Arguments of one frame preparation (device pointers of the destination slot).
+struct PrepArgs {
+    const float *raw;
+    int to_cm, downsample;
+    double focal;
+    double *depth_cm, *cx, *cy, *cz, *tmp, *ctb;
+    float *dt;
+    int *dtf;
+    PrepInfo *info;
+    DevObs *obs_out;
+    unsigned *ctr;  // [0] bands arrived, [1] (merged cloud, DT) arrived
+};
+
+// LDS layout: chunk[PREP_CH] doubles | acc1, flag (64 B) | wcnt, hcnt | mask bits | wmax
+constexpr int prep_lds_bytes() {
+    return PREP_CH * 8 + 64 + 2 * (PREP_NT / 64) * 4 + HPE_IMG_W * HPE_IMG_H / 32 * 4 + 64;
+}
 
 // inclusive prefix minimum over lanes 0..63 of a wave (DPP row shifts + row broadcasts)
 __device__ __forceinline__ int wave_prefix_min(int v) {
@@ -37,50 +67,59 @@ __device__ __forceinline__ int wave_prefix_min(int v) {
     v = min(v, __builtin_amdgcn_update_dpp(id, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
     return v;
 }
-
-// One chamfer row step over 320 columns held by threads 0..319 (5 waves): returns
-// T_j = min(a_j, T_{j-1} + HV) with T_{-1} = INIT, via a prefix minimum of a_j - HV*j.
-__device__ __forceinline__ int dt_row_scan(int a, int j, int *wmin) {
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    int v = wave_prefix_min(a - DT_HV * j);
-    if (l == 63 && w < 5) wmin[w] = v;
-    __syncthreads();
-    int pre = 0x7FFFFFFF;
-    for (int k = 0; k < w && k < 5; ++k) pre = min(pre, wmin[k]);
-    v = min(v, pre);
-    __syncthreads();
-    return min(v + DT_HV * j, DT_INIT + DT_HV * (j + 1));
+// value of lane l-1 (lane 0: fill) / lane l+1 (lane 63: fill)
+__device__ __forceinline__ int from_left(int v, int fill) {
+    return __builtin_amdgcn_update_dpp(fill, v, 0x138, 0xf, 0xf, false);  // wave_shr:1
+}
+__device__ __forceinline__ int from_right(int v, int fill) {
+    return __builtin_amdgcn_update_dpp(fill, v, 0x130, 0xf, 0xf, false);  // wave_shl:1
 }
 
-__global__ __launch_bounds__(PREP_NT) void k_preprocess(
-    const float *__restrict__ raw, int to_cm, int downsample, double focal,
-    double *__restrict__ depth_cm, float *__restrict__ dt, double *__restrict__ cx,
-    double *__restrict__ cy, double *__restrict__ cz, double *__restrict__ tmp,
-    double *__restrict__ ctb,
-    int *__restrict__ dtf, DevObs *__restrict__ obs_out, PrepInfo *__restrict__ info) {
-    constexpr int W = HPE_IMG_W, H = HPE_IMG_H, NPIX = W * H, NWV = PREP_NT / 64;
-    __shared__ int wcnt[NWV], hcnt[NWV];
-    __shared__ double wsum[NWV][2];
-    __shared__ double chunk[PREP_CH];
-    __shared__ int ring[3][W + 4];
-    __shared__ int wmin[8];
-    __shared__ float wmax[NWV];
+// Producer side of a hand-off, then the arrival; returns (to every thread) whether this
+// workgroup arrived last of `parties` (it then holds an agent acquire).
+__device__ __forceinline__ bool prep_arrive_last(unsigned *ctr, unsigned parties, int *flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores are out
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned old = atomicAdd(ctr, 1u);
+        const bool last = (old == parties - 1);
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            *ctr = 0u;  // ready for the next frame (the kernel boundary orders it)
+        }
+        *flag = last ? 1 : 0;
+    }
+    __syncthreads();
+    return *flag != 0;
+}
+
+// ---- band workgroup b: rows [30b, 30b + 30)
+__device__ __forceinline__ void prep_band(const PrepArgs &a, int b, unsigned char *lds) {
+    constexpr int W = HPE_IMG_W, NWV = PREP_NT / 64;
+    int *wcnt = (int *)(lds + PREP_CH * 8 + 64), *hcnt = wcnt + NWV;
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    const double focal = a.focal;
     const double c0 = 320 / 2., c1 = 240 / 2.;
     const double Kv[9] = {focal, 0.0, c0, 0.0, focal, c1, 0.0, 0.0, 1.0};
-    // ---- A: depth, cloud compaction (row-major), scale contributions; 1024 pixels a pass
+    const int pbase = b * PREP_BAND_PIX;
+    double *tmpb = a.tmp + 3 * (size_t)pbase, *ctbb = a.ctb + pbase;
     int base = 0, ncm = 0;
-    double acc0 = 0, acc1 = 0;  // threads 0 / 1: even / odd terms of the scale mean
-    for (int p0 = 0; p0 < NPIX; p0 += PREP_NT) {
-        const int pix = p0 + t;
-        const double Z = to_cm ? (double)raw[pix] / 10. : (double)raw[pix];
-        depth_cm[pix] = Z;
-        const bool nz = Z != 0;
-        const unsigned long long b = __ballot(nz);
-        const int wpre = __popcll(b & ((1ull << l) - 1));
-        double contrib = 0;
+    float rnext = a.raw[pbase + t];  // one pass ahead: the load latency hides under the pass
+    for (int p0 = 0; p0 < PREP_BAND_PIX; p0 += PREP_NT) {
+        const int q = p0 + t, pix = pbase + q;
+        const bool in = q < PREP_BAND_PIX;
+        const float rv = rnext;
+        if (q + PREP_NT < PREP_BAND_PIX) rnext = a.raw[pix + PREP_NT];
+        const double Z = a.to_cm ? (double)rv / 10. : (double)rv;
+        if (in) a.depth_cm[pix] = Z;
+        const bool nz = in && Z != 0;
+        const unsigned long long bm = __ballot(nz);
+        const int wpre = __popcll(bm & ((1ull << l) - 1));
+        double contrib = 0, X = 0, Y = 0;
         bool has = false;
-        double X = 0, Y = 0;
         if (nz) {
             const int r = pix / W, c = pix - W * r;
             X = ((c - c0) * Z) / focal;
@@ -103,11 +142,12 @@ __global__ __launch_bounds__(PREP_NT) void k_preprocess(
         const unsigned long long bh = __ballot(has);
         const int hpre = __popcll(bh & ((1ull << l) - 1));
         if (l == 0) {
-            wcnt[w] = __popcll(b);
+            wcnt[w] = __popcll(bm);
             hcnt[w] = __popcll(bh);
         }
         __syncthreads();
         int off = base, hoff = ncm, tot = 0, htot = 0;
+#pragma unroll
         for (int k = 0; k < NWV; ++k) {
             off += (k < w) ? wcnt[k] : 0;
             hoff += (k < w) ? hcnt[k] : 0;
@@ -116,125 +156,242 @@ __global__ __launch_bounds__(PREP_NT) void k_preprocess(
         }
         if (nz) {
             const int idx = off + wpre;
-            tmp[3 * idx + 0] = X;
-            tmp[3 * idx + 1] = Y * -1;
-            tmp[3 * idx + 2] = Z * -1;
+            tmpb[3 * idx + 0] = X;
+            tmpb[3 * idx + 1] = Y * -1;
+            tmpb[3 * idx + 2] = Z * -1;
         }
-        if (has) ctb[hoff + hpre] = contrib;  // the mean's terms, in pixel order
+        if (has) ctbb[hoff + hpre] = contrib;  // the mean's terms, in pixel order
         base += tot;
         ncm += htot;
         __syncthreads();
     }
-    const int n_full = base;
+    if (t == 0) {
+        a.info->band_n[b] = base;
+        a.info->band_h[b] = ncm;
+    }
+}
+
+// ---- merge (the last band to arrive): offsets, the scale mean, the (down-sampled) cloud
+__device__ __forceinline__ void prep_merge(const PrepArgs &a, unsigned char *lds) {
+    double *chunk = (double *)lds;
+    double *acc1p = chunk + PREP_CH;
+    const int t = threadIdx.x;
+    int noff[PREP_BANDS + 1], hoff[PREP_BANDS + 1];
+    noff[0] = hoff[0] = 0;
+#pragma unroll
+    for (int b = 0; b < PREP_BANDS; ++b) {
+        noff[b + 1] = noff[b] + a.info->band_n[b];
+        hoff[b + 1] = hoff[b] + a.info->band_h[b];
+    }
+    const int n_full = noff[PREP_BANDS], ncm = hoff[PREP_BANDS];
     // arma::mean = accumulate / n: two accumulators take the terms alternately, each a
     // sequential sum (arrayops::accumulate); threads 0 and 1 replay them from LDS chunks
+    double acc = 0;
     for (int b0 = 0; b0 < ncm; b0 += PREP_CH) {
         const int m = min(PREP_CH, ncm - b0);
-        for (int k = t; k < m; k += PREP_NT) chunk[k] = ctb[b0 + k];
+        for (int k = t; k < m; k += PREP_NT) {
+            const int g = b0 + k;
+            int b = 0;
+#pragma unroll
+            for (int q = 1; q < PREP_BANDS; ++q) b = (g >= hoff[q]) ? q : b;
+            chunk[k] = a.ctb[(size_t)b * PREP_BAND_PIX + (g - hoff[b])];
+        }
         __syncthreads();
-        if (t < 2) {
-            double a = (t == 0) ? acc0 : acc1;
-            for (int k = (b0 + t) & 1 ? 1 : 0; k < m; k += 2) a += chunk[k];
-            if (t == 0) acc0 = a;
-            else acc1 = a;
+        if (t < 2) {  // eight LDS reads in flight ahead of the dependent adds
+            int k = ((b0 + t) & 1) ? 1 : 0;
+            for (; k + 14 < m; k += 16) {
+                double v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = chunk[k + 2 * u];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) acc += v[u];
+            }
+            for (; k < m; k += 2) acc += chunk[k];
         }
         __syncthreads();
     }
-    if (t == 1) wsum[0][1] = acc1;
-    __syncthreads();
-    if (t == 0) acc1 = wsum[0][1];
-    // ---- B: down-sample (observedmodel.cpp:204-217) into the slot's SoA cloud
-    const int n = downsample ? 250 : n_full;
+    if (t == 1) *acc1p = acc;
+    const int n = a.downsample ? 250 : n_full;
     const int f = n_full / 250;
     for (int k = t; k < n; k += PREP_NT) {
         double x = 0, y = 0, z = 0;
-        const int src = downsample ? k * f : k;
-        if (!downsample || n_full > 0) {
-            x = tmp[3 * src + 0];
-            y = tmp[3 * src + 1];
-            z = tmp[3 * src + 2];
+        const int src = a.downsample ? k * f : k;
+        if (!a.downsample || n_full > 0) {
+            int b = 0;
+#pragma unroll
+            for (int q = 1; q < PREP_BANDS; ++q) b = (src >= noff[q]) ? q : b;
+            const double *p = a.tmp + 3 * ((size_t)b * PREP_BAND_PIX + (src - noff[b]));
+            x = p[0];
+            y = p[1];
+            z = p[2];
         }
-        cx[k] = x;
-        cy[k] = y;
-        cz[k] = z;
+        a.cx[k] = x;
+        a.cy[k] = y;
+        a.cz[k] = z;
     }
-    // ---- C: distance transform, rows in sequence, columns in parallel (threads < 320)
-    const bool col = t < W;
-    for (int k = t; k < 3 * (W + 4); k += PREP_NT) (&ring[0][0])[k] = DT_INIT;
-    __syncthreads();
-    // forward pass (mask rows r-2, r-1 and the left neighbour)
-    double dnext = col ? depth_cm[t] : 0.0;
-    for (int r = 0; r < H; ++r) {
-        const double dcur = dnext;
-        if (col && r + 1 < H) dnext = depth_cm[(r + 1) * W + t];
-        int a = 0;
-        if (col && dcur == 0) {
-            const int *u2 = ring[(r + 1) % 3], *u1 = ring[(r + 2) % 3];  // rows r-2, r-1
-            const int j = t + 2;
-            a = min(min(min(u2[j - 1] + DT_LONG, u2[j + 1] + DT_LONG),
-                        min(u1[j - 2] + DT_LONG, u1[j - 1] + DT_DIAG)),
-                    min(min(u1[j] + DT_HV, u1[j + 1] + DT_DIAG), u1[j + 2] + DT_LONG));
-        }
-        const int T = dt_row_scan(col ? a : 0x3FFFFFFF, t, wmin);
-        if (col) {
-            ring[r % 3][t + 2] = T;
-            dtf[r * W + t] = T;
-        }
-        __syncthreads();
-    }
-    // backward pass (rows r+1, r+2 and the right neighbour): column c = W-1-t
-    for (int k = t; k < 3 * (W + 4); k += PREP_NT) (&ring[0][0])[k] = DT_INIT;
-    __syncthreads();
-    const int c = W - 1 - t;
-    float mx = 0.f;
-    int fnext = col ? dtf[(H - 1) * W + c] : 0;
-    const float sc = 1.f / 65536;
-    for (int r = H - 1; r >= 0; --r) {
-        const int fcur = fnext;
-        if (col && r > 0) fnext = dtf[(r - 1) * W + c];
-        int b = 0;
-        if (col) {
-            const int *d1 = ring[(r + 1) % 3], *d2 = ring[(r + 2) % 3];  // rows r+1, r+2
-            const int j = c + 2;
-            b = min(min(min(fcur, d2[j + 1] + DT_LONG), min(d2[j - 1] + DT_LONG, d1[j + 2] + DT_LONG)),
-                    min(min(d1[j + 1] + DT_DIAG, d1[j] + DT_HV),
-                        min(d1[j - 1] + DT_DIAG, d1[j - 2] + DT_LONG)));
-        }
-        const int T = dt_row_scan(col ? b : 0x3FFFFFFF, t, wmin);
-        if (col) {
-            ring[r % 3][c + 2] = T;
-            const float v = (float)T * sc;
-            dt[r * W + c] = v;
-            mx = v > mx ? v : mx;
-        }
-        __syncthreads();
-    }
-    // ---- D: max(DT), the frame descriptor
-    for (int off = 32; off > 0; off >>= 1) {
-        const float o = __shfl_xor(mx, off);
-        mx = o > mx ? o : mx;
-    }
-    if (l == 0) wmax[w] = mx;
     __syncthreads();
     if (t == 0) {
-        float m = wmax[0];
-        for (int k = 1; k < NWV; ++k) m = wmax[k] > m ? wmax[k] : m;
-        const double scale = ncm ? (acc0 + acc1) / ncm : __builtin_nan("");
-        DevObs od;
-        od.cx = cx;
-        od.cy = cy;
-        od.cz = cz;
-        od.depth = depth_cm;
-        od.dt = dt;
-        od.n = n;
-        od.lambda = (double)HPE_NS / (double)n;  // costfunc.cpp:372
-        od.scale = scale;
-        od.dtmax = m;
-        for (int k = 0; k < 9; ++k) od.K[k] = Kv[k];
-        *obs_out = od;
-        info->n_full = n_full;
-        info->n = n;
-        info->scale = scale;
-        info->dtmax = m;
+        a.info->n_full = n_full;
+        a.info->n = n;
+        a.info->scale = ncm ? (acc + *acc1p) / ncm : __builtin_nan("");
     }
+}
+
+// ---- DT workgroup: mask bits by all waves, the raster scans by wave 0
+__device__ __forceinline__ void prep_dt(const PrepArgs &a, unsigned char *lds) {
+    constexpr int W = HPE_IMG_W, H = HPE_IMG_H;
+    unsigned *msk = (unsigned *)(lds + PREP_CH * 8 + 64 + 2 * (PREP_NT / 64) * 4);
+    float *wmaxp = (float *)(msk + W * H / 32);
+    const int t = threadIdx.x, l = t & 63;
+    for (int p0 = 0; p0 < W * H; p0 += 4 * PREP_NT) {  // hand = non-zero raw depth
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int pix = p0 + q * PREP_NT + t;
+            v[q] = (pix < W * H) ? a.raw[pix] : 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const unsigned long long bm = __ballot(v[q] != 0.f);
+            const int pix = p0 + q * PREP_NT + t;
+            if ((l & 31) == 0 && pix < W * H) msk[pix >> 5] = (unsigned)(bm >> (l & 32));
+        }
+    }
+    if (t == 0) msk[W * H / 32] = 0u;  // the two-word window of the last pixels
+    __syncthreads();
+    if (t < 64) {
+        // forward pass: lane l owns columns c0..c0+4; u1 / u2 = rows r-1 / r-2 at columns
+        // c0-2 .. c0+6 (halo from the neighbour lanes)
+        const int c0 = 5 * l;
+        int u1[9], u2[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) u1[i] = u2[i] = DT_INIT;
+#pragma unroll 2
+        for (int r = 0; r < H; ++r) {
+            const int pix0 = r * W + c0;
+            const unsigned long long mw =
+                ((unsigned long long)msk[(pix0 >> 5) + 1] << 32) | msk[pix0 >> 5];
+            const unsigned hb = (unsigned)(mw >> (pix0 & 31));
+            int pm = 0x7FFFFFFF, p[5];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                const int i = k + 2;
+                // grouped by weight: min over the LONG, DIAG and HV neighbours, then the add
+                const int mL = min(min(u2[i - 1], u2[i + 1]), min(u1[i - 2], u1[i + 2]));
+                const int mD = min(u1[i - 1], u1[i + 1]);
+                int av = min(min(mL + DT_LONG, mD + DT_DIAG), u1[i] + DT_HV);
+                av = ((hb >> k) & 1u) ? 0 : av;
+                pm = min(pm, av - DT_HV * (c0 + k));
+                p[k] = pm;
+            }
+            const int ex = from_left(wave_prefix_min(pm), 0x7FFFFFFF);  // lanes < l
+            int T[5];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                const int c = c0 + k;
+                T[k] = min(min(p[k], ex) + DT_HV * c, DT_INIT + DT_HV * (c + 1));
+                a.dtf[pix0 + k] = T[k];
+            }
+#pragma unroll
+            for (int i = 0; i < 9; ++i) u2[i] = u1[i];
+            u1[0] = from_left(T[3], DT_INIT);
+            u1[1] = from_left(T[4], DT_INIT);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) u1[k + 2] = T[k];
+            u1[7] = from_right(T[0], DT_INIT);
+            u1[8] = from_right(T[1], DT_INIT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        // backward pass: lane l owns columns cb-k (cb = 319 - 5l, k = 0..4), i.e. scan
+        // index j = 5l + k; d1 / d2 = rows r+1 / r+2 at scan positions j-2 .. j+6
+        const int cb = W - 1 - 5 * l;
+        int d1[9], d2[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) d1[i] = d2[i] = DT_INIT;
+        float mx = 0.f;
+        const float sc = 1.f / 65536;
+        int fw[5], fn[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) fw[k] = a.dtf[(H - 1) * W + cb - k];
+#pragma unroll 2
+        for (int r = H - 1; r >= 0; --r) {
+#pragma unroll
+            for (int k = 0; k < 5; ++k) fn[k] = (r > 0) ? a.dtf[(r - 1) * W + cb - k] : 0;
+            int pm = 0x7FFFFFFF, p[5];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                const int i = k + 2;
+                const int mL = min(min(d2[i - 1], d2[i + 1]), min(d1[i - 2], d1[i + 2]));
+                const int mD = min(d1[i - 1], d1[i + 1]);
+                const int bv = min(min(fw[k], mL + DT_LONG), min(mD + DT_DIAG, d1[i] + DT_HV));
+                pm = min(pm, bv - DT_HV * (5 * l + k));
+                p[k] = pm;
+            }
+            const int ex = from_left(wave_prefix_min(pm), 0x7FFFFFFF);
+            int T[5];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                const int j = 5 * l + k;
+                T[k] = min(min(p[k], ex) + DT_HV * j, DT_INIT + DT_HV * (j + 1));
+                const float v = (float)T[k] * sc;
+                a.dt[r * W + cb - k] = v;
+                mx = v > mx ? v : mx;
+            }
+#pragma unroll
+            for (int i = 0; i < 9; ++i) d2[i] = d1[i];
+            d1[0] = from_left(T[3], DT_INIT);
+            d1[1] = from_left(T[4], DT_INIT);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) d1[k + 2] = T[k];
+            d1[7] = from_right(T[0], DT_INIT);
+            d1[8] = from_right(T[1], DT_INIT);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) fw[k] = fn[k];
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            const float o = __shfl_xor(mx, off);
+            mx = o > mx ? o : mx;
+        }
+        if (l == 0) *wmaxp = mx;
+    }
+    __syncthreads();
+    if (t == 0) a.info->dtmax = *wmaxp;
+}
+
+// The frame descriptor every tracking kernel reads.
+__device__ __forceinline__ void prep_write_descriptor(const PrepArgs &a) {
+    const PrepInfo *pi = a.info;
+    DevObs od;
+    od.cx = a.cx;
+    od.cy = a.cy;
+    od.cz = a.cz;
+    od.depth = a.depth_cm;
+    od.dt = a.dt;
+    od.n = pi->n;
+    od.lambda = (double)HPE_NS / (double)pi->n;  // costfunc.cpp:372
+    od.scale = pi->scale;
+    od.dtmax = pi->dtmax;
+    const double Kv[9] = {a.focal, 0.0, 320 / 2., 0.0, a.focal, 240 / 2., 0.0, 0.0, 1.0};
+    for (int k = 0; k < 9; ++k) od.K[k] = Kv[k];
+    *a.obs_out = od;
+}
+
+// One preparing workgroup (index g in [0, PREP_WG)); the last to finish writes the
+// descriptor.
+__device__ __forceinline__ void prep_workgroup(const PrepArgs &a, int g, unsigned char *lds) {
+    int *flag = (int *)(lds + PREP_CH * 8 + 8);
+    if (g < PREP_BANDS) {
+        prep_band(a, g, lds);
+        if (!prep_arrive_last(a.ctr, PREP_BANDS, flag)) return;
+        prep_merge(a, lds);
+    } else {
+        prep_dt(a, lds);
+    }
+    if (prep_arrive_last(a.ctr + 1, 2, flag) && threadIdx.x == 0) prep_write_descriptor(a);
+}
+
+__global__ __launch_bounds__(PREP_NT) void k_prepare(PrepArgs a) {
+    __shared__ __align__(16) unsigned char lds[prep_lds_bytes()];
+    prep_workgroup(a, blockIdx.x, lds);
 }

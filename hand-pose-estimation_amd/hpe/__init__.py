@@ -96,6 +96,21 @@ class Context:
         self.check(self.lib.hpe_prepare_frame(self._h, slot, ptr(d, C.c_float), int(to_cm),
                                               int(downsample), float(focal)))
 
+    def pipeline_begin(self, depth_mm, to_cm=True, downsample=True, focal=241.42):
+        d = np.ascontiguousarray(depth_mm, dtype=np.float32).reshape(IMG_H, IMG_W)
+        self.check(self.lib.hpe_pipeline_begin(self._h, ptr(d, C.c_float), int(to_cm),
+                                               int(downsample), float(focal)))
+
+    def track_pipelined(self, num_p, refine, d_state_ptr, next_depth_mm=None):
+        """Track the pipeline's current frame into the 27 device doubles at d_state_ptr and
+        prepare next_depth_mm (host) as the following frame."""
+        nd = None
+        if next_depth_mm is not None:
+            nd = np.ascontiguousarray(next_depth_mm, dtype=np.float32).reshape(IMG_H, IMG_W)
+        self.check(self.lib.hpe_track_pipelined(self._h, int(num_p), int(refine),
+                                                C.c_void_p(d_state_ptr),
+                                                ptr(nd, C.c_float) if nd is not None else None))
+
     def frame_readback(self, slot):
         depth = np.zeros((IMG_H, IMG_W)); dt = np.zeros((IMG_H, IMG_W), dtype=np.float32)
         cloud = np.zeros((IMG_H * IMG_W, 3)); n = C.c_int32(0)

@@ -167,6 +167,18 @@ int hpe_track_frame(hpe_ctx *ctx, int num_p, int refine, double x0_inout[26],
  * hpe_stream(ctx): no host synchronisation. */
 int hpe_track_frame_dev(hpe_ctx *ctx, int num_p, int refine, double *d_state);
 
+/* Pipelined tracking: test_full's loop (testmodel.cpp:117-139) with next_frame
+ * (observedmodel.cpp:420-430) of frame f+1 running INSIDE frame f's refine launch, on CUs
+ * the single-workgroup refine leaves idle: one stream, one replayed graph per frame.
+ * hpe_pipeline_begin prepares the first raw depth frame (float mm, 240x320, host).
+ * hpe_track_pipelined tracks the current frame exactly like hpe_track_frame_dev
+ * (d_state: 27 device doubles {x0 -> bestp, cost}) and, if next_depth_mm != NULL, copies
+ * it (host) and prepares it as the next current frame; NULL ends the sequence. */
+int hpe_pipeline_begin(hpe_ctx *ctx, const float *depth_mm, int to_cm, int downsample,
+                       double focal);
+int hpe_track_pipelined(hpe_ctx *ctx, int num_p, int refine, double *d_state,
+                        const float *next_depth_mm);
+
 /* Kernel timing with HIP events on the context stream (bench instrumentation).
  * While enabled, every dispatch of the profiled kernels is launched through
  * hipExtLaunchKernel with a start/stop event pair (dispatch-packet timestamps: the
@@ -175,10 +187,11 @@ int hpe_track_frame_dev(hpe_ctx *ctx, int num_p, int refine, double *d_state);
  * device milliseconds of one kernel since the last enable; hpe_profile_read is
  * hpe_profile_read_kernel(HPE_PROF_PSO_GEN). */
 #define HPE_PROF_PSO_GEN 0   /* k_pso_gen: one fused PSO generation */
-#define HPE_PROF_REFINE 1    /* k_refine: refine_init_pose */
+#define HPE_PROF_REFINE 1    /* k_refine: refine_init_pose (+ fused next-frame preparation) */
 #define HPE_PROF_PSO_INIT 2  /* k_pso_init */
 #define HPE_PROF_PSO_FINAL 3 /* k_pso_final */
-#define HPE_PROF_KERNELS 4
+#define HPE_PROF_PREP 4      /* k_preprocess (hpe_prepare_frame, preprocessing stream) */
+#define HPE_PROF_KERNELS 5
 int hpe_profile_enable(hpe_ctx *ctx, int on);
 int hpe_profile_read(hpe_ctx *ctx, int32_t *launches, double *total_ms, double *min_ms,
                      double *max_ms);

@@ -16,6 +16,12 @@ for p in (ROOT, PKG, ROOT / "oracle", ROOT / "tests"):
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a gfx950 GPU (run with -m gpu)")
+    mark = config.getoption("-m") or ""
+    if "gpu" in mark and "not gpu" not in mark:
+        # torch's HIP runtime must initialise before libhpe.so's (tests that hand torch
+        # device buffers to the ABI)
+        import torch
+        torch.cuda.is_available()
 
 
 @pytest.fixture(scope="session")

@@ -81,3 +81,39 @@ def test_prepared_frames_track_like_oracle(gh, oracle, ora_hand, np_hand):
         cr = oracle.cal_cost(ora_hand, obs, x_ref)
         np.testing.assert_allclose(x_gpu, x_ref, rtol=0, atol=1e-6)
         assert abs(cost.value - cr) <= 1e-8 * abs(cr)
+
+
+@pytest.mark.parametrize("downsample", [True, False])
+def test_pipelined_tracking_like_oracle(gh, oracle, ora_hand, np_hand, downsample):
+    """hpe_track_pipelined: each frame is prepared inside the previous frame's refine launch
+    (fused workgroups); the tracked poses / costs must equal the oracle's test_full loop on
+    the same raw frames."""
+    import ctypes as C
+    import hpe
+    poses = hand_data.trajectory(4, seed=19)
+    depth = [oracle_np.render_depth_mm(np_hand, th) for th in poses]
+    ub, lb, sd = oracle_np.reference_bounds()
+    maxiter = 6 if downsample else 3
+    P = 32 if downsample else 8
+    pso = hpe.PSO()
+    pso.set_pso_params(ub, lb, sd, 0.7298, 1.49618, 1.49618, maxiter, 1e-8, 1e-8)
+    pso._push(gh.ctx)
+    state = np.zeros(27)
+    dbuf = C.c_void_p()
+    rt = gh.ctx.lib
+    import torch
+    st = torch.zeros(27, dtype=torch.float64, device="cuda:0")
+    st[:26] = torch.from_numpy(oracle_np.X0)
+    torch.cuda.synchronize()
+    gh.ctx.pipeline_begin(depth[0], downsample=downsample)
+    x_ref = oracle_np.X0.copy()
+    for f in range(4):
+        gh.ctx.track_pipelined(P, 1, st.data_ptr(), depth[f + 1] if f + 1 < 4 else None)
+        gh.ctx.check(rt.hpe_sync(gh.ctx.h))
+        out = st.cpu().numpy()
+        obs = oracle.preprocess(depth[f], downsample=downsample)
+        x_ref, _ = oracle.refine(ora_hand, obs, x_ref)
+        x_ref, _, _ = oracle.pso_evolve(ora_hand, obs, x_ref, P, maxiter, lb, ub, sd)
+        cr = oracle.cal_cost(ora_hand, obs, x_ref)
+        np.testing.assert_allclose(out[:26], x_ref, rtol=0, atol=1e-6)
+        assert abs(out[26] - cr) <= 1e-8 * abs(cr)

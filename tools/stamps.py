@@ -5,6 +5,9 @@ import sys
 from pathlib import Path
 
 import numpy as np
+import torch
+
+torch.cuda.set_device(0)  # torch's HIP runtime first
 
 ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT / "hand-pose-estimation_amd"))
@@ -33,7 +36,8 @@ names = {4: "gen: prologue (og + hand)", 5: "gen: block-0 span (cycles)",
          13: "fk: trig phase", 14: "fk: chain+spheres phase", 15: "wave: depth issue",
          16: "wave: align frozen", 17: "wave: collision", 18: "wave: 3 reductions",
          20: "refine: corr eval", 21: "refine: grad evals", 22: "refine: goldstein",
-         23: "refine: iter glue"}
+         23: "refine: iter glue", 24: "prep (fused): band workgroups (incl. merge)",
+         25: "prep (fused): DT workgroup"}
 tot = np.zeros(64)
 for f in range(1, nfr + 1):
     ctx.select_frame(f)
@@ -41,6 +45,17 @@ for f in range(1, nfr + 1):
     ctx.check(lib.hpe_sync(ctx.h))
     rc = lib.hpe_debug_stamps(st.ctypes.data_as(C.POINTER(C.c_uint64)))
     tot += st
+# pipelined frames: next-frame preparation fused into the refine launch
+import torch  # noqa: E402
+raw = [np.ascontiguousarray(ctx.render_depth(th)) for th in poses]
+stt = torch.zeros(27, dtype=torch.float64, device="cuda:0")
+stt[:26] = torch.from_numpy(poses[0])
+ctx.pipeline_begin(raw[0])
+for f in range(nfr):
+    ctx.track_pipelined(P, 1, stt.data_ptr(), raw[f + 1])
+ctx.check(lib.hpe_sync(ctx.h))
+lib.hpe_debug_stamps(st.ctypes.data_as(C.POINTER(C.c_uint64)))
+tot[24] += st[24]; tot[25] += st[25]; tot[56] += st[56]; tot[57] += st[57]
 print("stamps build:", rc)
 for k, nm in names.items():
     n = tot[32 + k]
