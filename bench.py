@@ -211,8 +211,18 @@ def main():
     ctx.check(lib.hpe_profile_enable(ctx.h, 1))
     if not args.resident:
         ctx.pipeline_begin(raw[args.warmup], True, ds)
+    errs = []  # gnd_truth_err (costfunc.cpp:476-507) of each frame's bestp vs the true pose
     for f in range(args.warmup, n_frames):
         step(f)
+        ctx.check(lib.hpe_sync(ctx.h))
+        torch.cuda.synchronize()
+        bp = state[:26].cpu().numpy()
+        hand.build_hand_model(bp)
+        est = hand.hand_joints.copy()
+        hand.build_hand_model(poses[f])
+        gt = hand.hand_joints * 10.0
+        gt[:, 1:3] *= -1
+        errs.append(hpe.gnd_truth_err(est, gt.ravel()))
     ctx.check(lib.hpe_sync(ctx.h))
     prof = {}
     for name, kid in (("k_pso_gen", 0), ("k_refine", 1), ("k_pso_init", 2), ("k_pso_final", 3),
@@ -262,6 +272,10 @@ def main():
                    "parallelism": f"subswarms x{world}, all-gather best per frame"},
         "tracked_fps": args.steps / el,
         "final_cost": float(final[26]),
+        "tracking_err_mm": {"sum_wrist_tips_mean": float(np.mean(errs)),
+                            "per_joint_mean": float(np.mean(errs) / 6),
+                            "note": "gnd_truth_err (costfunc.cpp:476-507) vs the synthetic "
+                                    "trajectory's true poses, second pass over the frames"},
         "roofline": {
             "bound": "hbm", "kernel": "k_pso_gen",
             "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

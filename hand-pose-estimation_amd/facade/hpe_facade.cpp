@@ -3,6 +3,7 @@
 // gfx950 kernels.  Reference semantics are cited per method (/root/reference/src).
 #include "hpe_facade.hpp"
 
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -397,6 +398,27 @@ double costfunc::depth_penalty(arma::mat &, arma::mat &, arma::mat &spheres, arm
 double costfunc::self_collision_penalty(arma::mat &spheresM, arma::vec &) {
     // costfunc.cpp:130-197 (the hand's radii)
     return sphere_term(spheresM, nullptr, 2);
+}
+
+double costfunc::gnd_truth_err(arma::mat &gnd_truth, int frame) {
+    // costfunc.cpp:476-507 on the host joints of the last build_hand_model (evaluation only)
+    if (gnd_truth.n_cols != 63 || frame < 0 || (arma::uword)frame >= gnd_truth.n_rows)
+        throw std::invalid_argument("gnd_truth: frames x 63");
+    const arma::mat &hj = hand->hand_joints;
+    double d[6];
+    const int sel[6] = {0, 4, 8, 12, 16, 20};
+    for (int q = 0; q < 6; ++q) {
+        const int j = sel[q];
+        double e[3];
+        for (int r = 0; r < 3; ++r) {
+            double v = hj(j, r) * 10.0;  // back to mm
+            if (r > 0) v *= -1;          // hand_joints.cols(1,2) *= -1
+            e[r] = gnd_truth(frame, 3 * j + r) - v;
+        }
+        d[q] = std::sqrt((e[0] * e[0] + e[1] * e[1]) + e[2] * e[2]);
+    }
+    // sum(): arrayops::accumulate, two alternating accumulators
+    return ((d[0] + d[2]) + d[4]) + ((d[1] + d[3]) + d[5]);
 }
 
 // ------------------------------------------------------------------ PSO

@@ -138,6 +138,10 @@ public:
     double self_collision_penalty(arma::mat &spheresM, arma::vec &spheresR);
     void compute_correspondences(arma::mat &ptns, arma::mat &sphM, arma::uvec &matchId);
     arma::uvec get_matchIdx() const { return matchIdx; }
+    // costfunc.cpp:476-507: wrist + five finger tips error (mm) of the hand_joints left by
+    // the last build_hand_model against row `frame` of gnd_truth (frames x 63, joint j at
+    // columns 3j..3j+2)
+    double gnd_truth_err(arma::mat &gnd_truth, int frame);
 
     // --- extensions: the OpenMP particle loops of PSO.cpp:748,848 as one launch
     void cal_cost_batch(arma::mat &thetas, arma::vec &costs, bool with_collision = false);

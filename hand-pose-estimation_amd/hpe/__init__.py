@@ -18,6 +18,7 @@ from . import _lib
 from ._lib import HpeError, ptr
 
 __all__ = ["handmodel", "observedmodel", "costfunc", "PSO", "reference_hand", "HpeError",
+           "gnd_truth_err",
            "Context", "preprocess_depth", "reference_bounds", "X0"]
 
 IMG_H, IMG_W = 240, 320
@@ -284,6 +285,11 @@ class costfunc:
         self.last_terms = terms
         return cost.value
 
+    def gnd_truth_err(self, gnd_truth, frame):
+        """costfunc.cpp:476-507: wrist + finger-tip error (mm) of the hand_joints left by the
+        last build_hand_model against row `frame` of gnd_truth (frames x 63)."""
+        return gnd_truth_err(self.hand.hand_joints, np.asarray(gnd_truth)[frame])
+
     # ---- term-level API on a sphere matrix (costfunc.cpp:130-377), one launch each
     def _sphere_terms(self, spheres, matchId=None):
         self._sync_frame()
@@ -326,6 +332,18 @@ class costfunc:
     def self_collision_penalty(self, spheresM, spheresR):
         """costfunc.cpp:130-197: adjacent-digit sphere overlap penalty."""
         return float(self._sphere_terms(spheresM)[0][2])
+
+
+def gnd_truth_err(hand_joints, gt_row):
+    """costfunc.cpp:476-507 for one frame: gt_row holds 63 values (joint j at 3j..3j+2, mm);
+    hand_joints is the (21, 3) cm matrix of build_hand_model (handmodel.cpp:291-296)."""
+    gt = np.asarray(gt_row, dtype=np.float64).reshape(21, 3)
+    hj = np.asarray(hand_joints, dtype=np.float64) * 10.0
+    hj[:, 1:3] *= -1
+    e = gt - hj
+    d = [float(np.sqrt((e[j, 0] * e[j, 0] + e[j, 1] * e[j, 1]) + e[j, 2] * e[j, 2]))
+         for j in (0, 4, 8, 12, 16, 20)]
+    return ((d[0] + d[2]) + d[4]) + ((d[1] + d[3]) + d[5])
 
 
 class PSO:

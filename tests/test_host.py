@@ -118,3 +118,17 @@ def test_facade_missing_bin_aborts(facade_host):
     out = subprocess.run([str(facade_host), "abort"], capture_output=True, text=True, timeout=60)
     assert out.returncode == -signal.SIGABRT
     assert "open file for input failed" in out.stderr
+
+
+def test_gnd_truth_err_host():
+    """costfunc.cpp:476-507 restated on the host joints: zero at the true pose, and the
+    six-joint sum for a known offset."""
+    import hpe
+    rng = np.random.default_rng(0)
+    hj = rng.normal(size=(21, 3))
+    gt = hj * 10.0
+    gt[:, 1:3] *= -1
+    assert hpe.gnd_truth_err(hj, gt.ravel()) == 0.0
+    gt2 = gt.copy()
+    gt2[[0, 4, 8, 12, 16, 20], 0] += 3.0  # 3 mm along x on the wrist and the five tips
+    assert abs(hpe.gnd_truth_err(hj, gt2.ravel()) - 18.0) < 1e-12
