@@ -369,7 +369,8 @@ double ora_u01(uint64_t seed, uint32_t stream, uint32_t gen, uint32_t idx, uint3
     return (double)u53 * 0x1.0p-53;
 }
 
-enum { ST_NORMAL = 1, ST_RP = 2, ST_RG = 3, ST_LINK = 4 };
+enum { ST_NORMAL = 1, ST_RP = 2, ST_RG = 3, ST_LINK = 4, ST_OPT_PERM = 5, ST_OPT_RP = 6,
+       ST_OPT_RG = 7, ST_OPT_NORMAL = 8 };
 
 /* randn<mat>(26, P) replacement: Box-Muller on Philox pairs (dims 2q, 2q+1) */
 void ora_normals(uint64_t seed, int P, double *out) {
@@ -382,6 +383,19 @@ void ora_normals(uint64_t seed, int P, double *out) {
             out[ORA_DOF * i + 2 * q] = r * cos(t);
             out[ORA_DOF * i + 2 * q + 1] = r * sin(t);
         }
+}
+
+/* Col::min(index): op_min::direct_min starts from +inf and keeps the first strict
+ * minimum, so NaN entries are skipped and an all-NaN/inf vector yields index 0. */
+static int arma_argmin(const double *v, int n) {
+    double best = INFINITY;
+    int id = 0;
+    for (int i = 0; i < n; ++i)
+        if (v[i] < best) {
+            best = v[i];
+            id = i;
+        }
+    return id;
 }
 
 /* check_constraints, PSO.cpp:358-377 (above-max clamps to MIN, :372) */
@@ -491,9 +505,7 @@ int ora_pso_evolve(const ora_hand *h, const ora_obs *o, const double x0[26], int
                 pc[i] = fx[i];
                 memcpy(pb + D * i, x + D * i, sizeof(double) * D);
             }
-        int fid = 0; /* pcost.min(fmin_id): first minimum, :864-865 */
-        for (int i = 1; i < P; ++i)
-            if (pc[i] < pc[fid]) fid = i;
+        const int fid = arma_argmin(pc, P); /* pcost.min(fmin_id), :864-865 */
         const double fmin = pc[fid];
         if (fmin < gcost) { /* gbest = particles.col(fmin_id), :869-873 */
             memcpy(gpos, x + D * fid, sizeof(gpos));
@@ -582,6 +594,117 @@ int ora_refine_init_pose(const ora_hand *h, const ora_obs *o, double x0[26]) {
     }
     free(match);
     return evals;
+}
+
+/* pso_optimise, PSO.cpp:539-712: each generation every particle first runs graditer = 10
+ * single-coordinate Goldstein steps (cal_gradient :380-405 on the coordinate permu(m),
+ * correspondences recomputed only at m = 0), then the global-best velocity update with
+ * w, c1, c2 and a cal_cost evaluation.  Quirks kept: pcost mixes cal_cost2 (descent) and
+ * cal_cost (update) values; gbest = particles.col(argmin pcost); the velocity zeroing on
+ * a descent improvement is undone by the write-back of the saved velocity (:628, :637).
+ * The reference draws from Armadillo without reseeding; here Philox streams 5..8. */
+int ora_pso_optimise(const ora_hand *h, const ora_obs *o, const double x0[26], int P,
+                     int maxiter, const double lb[26], const double ub[26],
+                     const double stdv[26], double w, double c1, double c2, uint64_t seed,
+                     double bestp[26], double *bestcost, double *gbest_trace, int nthreads) {
+    const int D = ORA_DOF, graditer = 10;
+    double *x = (double *)calloc((size_t)D * P, sizeof(double));
+    double *v = (double *)calloc((size_t)D * P, sizeof(double));
+    double *pb = (double *)calloc((size_t)D * P, sizeof(double));
+    double *pc = (double *)calloc((size_t)P, sizeof(double));
+    double *fx = (double *)calloc((size_t)P, sizeof(double));
+    double gpos[26], gcost = 1e100;
+    memset(gpos, 0, sizeof(gpos));
+    for (int i = 0; i < P; ++i) /* generate_particles(particles, x0, num_p, false) */
+        for (int q = 0; q < D / 2; ++q) {
+            const double u1 = ora_u01(seed, ST_OPT_NORMAL, 0, (uint32_t)i, 2u * q);
+            const double u2 = ora_u01(seed, ST_OPT_NORMAL, 0, (uint32_t)i, 2u * q + 1);
+            const double r = sqrt(-2.0 * log(1.0 - u1));
+            const double t = 6.283185307179586231995926937088370323181152343750 * u2;
+            x[D * i + 2 * q] = x0[2 * q] + (r * cos(t)) * stdv[2 * q];
+            x[D * i + 2 * q + 1] = x0[2 * q + 1] + (r * sin(t)) * stdv[2 * q + 1];
+        }
+    memcpy(pb, x, sizeof(double) * D * P);
+    ora_eval_costs(h, o, x, P, 0, pc, nthreads); /* :556-569 */
+    for (int i = 0; i < P; ++i)
+        if (pc[i] < gcost) {
+            gcost = pc[i];
+            memcpy(gpos, x + D * i, sizeof(gpos));
+        }
+    int count = 0;
+    for (int g = 1; g < maxiter; ++g) { /* iter 2..maxiter, :580-583 */
+#pragma omp parallel for num_threads(nthreads > 0 ? nthreads : omp_get_max_threads()) schedule(dynamic)
+        for (int i = 0; i < P; ++i) { /* descent, :592-639 */
+            int32_t *match = (int32_t *)malloc(sizeof(int32_t) * (o->n > 0 ? o->n : 1));
+            double th[26], vel[26];
+            memcpy(th, x + D * i, sizeof(th));
+            memcpy(vel, v + D * i, sizeof(vel));
+            for (int m = 0; m < graditer; ++m) {
+                const int corr = (m == 0);
+                const double fk = ora_cal_cost2(h, o, th, match, corr, NULL);
+                const double u = ora_u01(seed, ST_OPT_PERM, (uint32_t)g, (uint32_t)i, (uint32_t)m);
+                int sel = (int)floor(u * D);
+                if (sel > D - 1) sel = D - 1;
+                double grad[26], xph[26], xmh[26];
+                memcpy(xph, th, sizeof(xph));
+                memcpy(xmh, th, sizeof(xmh));
+                const double e = 1e-5;
+                xph[sel] += e;
+                xmh[sel] -= e;
+                const double fp = ora_cal_cost2(h, o, xph, match, 0, NULL);
+                const double fm = ora_cal_cost2(h, o, xmh, match, 0, NULL);
+                for (int d = 0; d < D; ++d) grad[d] = 0;
+                grad[sel] = (fp - fm) / (2 * e);
+                int ev = 0;
+                const double tk = goldstein(h, o, th, grad, match, fk, 30, &ev);
+                for (int d = 0; d < D; ++d) th[d] = th[d] - tk * grad[d];
+                const double f2 = ora_cal_cost2(h, o, th, match, corr, NULL);
+                if (f2 < pc[i]) {
+                    pc[i] = f2;
+                    memcpy(pb + D * i, th, sizeof(th));
+                }
+            }
+            check_constraints(th, vel, lb, ub);
+            memcpy(x + D * i, th, sizeof(th));
+            memcpy(v + D * i, vel, sizeof(vel));
+            free(match);
+        }
+        int fid = arma_argmin(pc, P); /* :643-650 */
+        if (pc[fid] < gcost) {
+            memcpy(gpos, x + D * fid, sizeof(gpos));
+            gcost = pc[fid];
+            count = 0;
+        }
+        for (int i = 0; i < P; ++i) { /* velocity / position, :652-677 */
+            double *xi = x + D * i, *vi = v + D * i;
+            const double *pbi = pb + D * i;
+            for (int d = 0; d < D; ++d) {
+                const double rp = ora_u01(seed, ST_OPT_RP, (uint32_t)g, (uint32_t)i, (uint32_t)d);
+                const double rg = ora_u01(seed, ST_OPT_RG, (uint32_t)g, (uint32_t)i, (uint32_t)d);
+                vi[d] = (w * vi[d] + (c1 * rp) * (pbi[d] - xi[d])) + (c2 * rg) * (gpos[d] - xi[d]);
+            }
+            for (int d = 0; d < D; ++d) xi[d] = xi[d] + vi[d];
+            check_constraints(xi, vi, lb, ub);
+        }
+        ora_eval_costs(h, o, x, P, 0, fx, nthreads); /* :679-689 */
+        for (int i = 0; i < P; ++i)
+            if (fx[i] < pc[i]) {
+                pc[i] = fx[i];
+                memcpy(pb + D * i, x + D * i, sizeof(double) * D);
+            }
+        fid = arma_argmin(pc, P); /* :692-704 */
+        if (pc[fid] < gcost) {
+            memcpy(gpos, x + D * fid, sizeof(gpos));
+            gcost = pc[fid];
+            count = 0;
+        } else
+            count += 1;
+        if (gbest_trace) gbest_trace[g - 1] = gcost;
+    }
+    memcpy(bestp, gpos, sizeof(gpos));
+    if (bestcost) *bestcost = gcost;
+    free(x); free(v); free(pb); free(pc); free(fx);
+    return 1;
 }
 
 /* ---------------- observation preprocessing ---------------- */

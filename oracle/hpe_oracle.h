@@ -89,6 +89,11 @@ int ora_pso_evolve(const ora_hand *h, const ora_obs *o, const double x0[26], int
 
 int ora_refine_init_pose(const ora_hand *h, const ora_obs *o, double x0[26]);
 
+int ora_pso_optimise(const ora_hand *h, const ora_obs *o, const double x0[26], int P,
+                     int maxiter, const double lb[26], const double ub[26],
+                     const double stdv[26], double w, double c1, double c2, uint64_t seed,
+                     double bestp[26], double *bestcost, double *gbest_trace, int nthreads);
+
 void ora_dist_transform(const double *depth_cm, float *dt_out);
 int ora_preprocess(const float *depth_mm, int to_cm, int downsample, double focal,
                    double *depth_cm_out, float *dt_out, double *cloud_out,

@@ -81,6 +81,10 @@ class Oracle:
         L.ora_normals.argtypes = [C.c_uint64, C.c_int, dp]
         L.ora_pso_evolve.argtypes = [C.POINTER(OraHand), C.POINTER(OraObs), dp, C.c_int, C.c_int,
                                      dp, dp, dp, C.c_uint64, dp, dp, C.POINTER(OraTrace), C.c_int]
+        L.ora_pso_optimise.argtypes = [C.POINTER(OraHand), C.POINTER(OraObs), dp, C.c_int,
+                                       C.c_int, dp, dp, dp, C.c_double, C.c_double, C.c_double,
+                                       C.c_uint64, dp, dp, dp, C.c_int]
+        L.ora_pso_optimise.restype = C.c_int
         L.ora_refine_init_pose.argtypes = [C.POINTER(OraHand), C.POINTER(OraObs), dp]
         L.ora_refine_init_pose.restype = C.c_int
         L.ora_dist_transform.argtypes = [dp, fp]
@@ -167,6 +171,20 @@ class Oracle:
         n = maxiter - 1
         return bp, bc.value, dict(gbest=tg[:n], fmin=tf[:n], count=tc[:n], topo=tt[:n],
                                   pcost0=p0)
+
+    def pso_optimise(self, h, obs, x0, P, maxiter, lb, ub, sd, w, c1, c2, seed=1000,
+                     nthreads=0):
+        """PSO.cpp:539-712 (descent + global-best PSO); returns bestp, gbest cost and the
+        gbest cost after each of the maxiter-1 generations."""
+        x = np.ascontiguousarray(x0, dtype=np.float64)
+        lb, ub, sd = (np.ascontiguousarray(a, dtype=np.float64) for a in (lb, ub, sd))
+        bp = np.zeros(26); bc = C.c_double(0)
+        tg = np.zeros(max(maxiter - 1, 1))
+        self.lib.ora_pso_optimise(C.byref(h), C.byref(obs.s), _p(x, C.c_double), P, maxiter,
+                                  _p(lb, C.c_double), _p(ub, C.c_double), _p(sd, C.c_double),
+                                  w, c1, c2, seed, _p(bp, C.c_double), C.byref(bc),
+                                  _p(tg, C.c_double), nthreads)
+        return bp, bc.value, tg[:max(maxiter - 1, 0)]
 
     def refine(self, h, obs, x0):
         x = np.array(x0, dtype=np.float64)

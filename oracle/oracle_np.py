@@ -243,6 +243,7 @@ def philox4x32_10(ctr, key):
 
 
 ST_NORMAL, ST_RP, ST_RG, ST_LINK = 1, 2, 3, 4
+ST_OPT_PERM, ST_OPT_RP, ST_OPT_RG, ST_OPT_NORMAL = 5, 6, 7, 8
 
 
 def u01(seed, stream, gen, idx, k):
@@ -307,6 +308,94 @@ def pso_evolve(hand, obs, x0, P, maxiter, lb, ub, sd, seed=1000, cost_fn=None):
             gpos, gcost, count = x[fid].copy(), pc[fid], 0
         else:
             count += 1
+        trace.append(gcost)
+    return gpos, gcost, trace
+
+
+def _goldstein(hand, obs, x, g, match, fk):
+    """PSO.cpp:438-480 with the default 30 iterations; returns tk."""
+    a, b, alpha = 0.0, 1e100, 0.5
+    p = -g
+    gp = float(np.dot(g, p))
+    for _ in range(30):
+        f1 = cal_cost2(hand, obs, x + alpha * p, match)[0]
+        if f1 <= fk + 0.25 * alpha * gp:
+            if f1 >= fk + 0.75 * alpha * gp:
+                return alpha
+            a = alpha
+            alpha = min(2 * alpha, 0.5 * (alpha + b))
+        else:
+            b = alpha
+            alpha = 0.5 * (a + alpha)
+    return 0.0
+
+
+def pso_optimise(hand, obs, x0, P, maxiter, lb, ub, sd, w, c1, c2, seed=1000):
+    """PSO.cpp:539-712: per generation, 10 single-coordinate Goldstein descent steps per
+    particle (cal_gradient :380-405), then the global-best velocity update.  Philox
+    streams 5..8 replace Armadillo's randi / randu / randn.  Returns (bestp, cost, trace)."""
+    nrm = np.zeros((P, 26))
+    for i in range(P):
+        for q in range(13):
+            u1 = u01(seed, ST_OPT_NORMAL, 0, i, 2 * q)
+            u2 = u01(seed, ST_OPT_NORMAL, 0, i, 2 * q + 1)
+            r = math.sqrt(-2.0 * math.log(1.0 - u1))
+            t = (2.0 * PI) * u2
+            nrm[i, 2 * q], nrm[i, 2 * q + 1] = r * math.cos(t), r * math.sin(t)
+    x = x0[None, :] + nrm * sd[None, :]
+    v = np.zeros_like(x)
+    pb = x.copy()
+    pc = np.array([cal_cost(hand, obs, x[i]) for i in range(P)])
+    gcost, gpos = 1e100, np.zeros(26)
+    for i in range(P):
+        if pc[i] < gcost:
+            gcost, gpos = pc[i], x[i].copy()
+    trace = []
+
+    def clamp(xi, vi):
+        lo = xi < lb; hi = xi > ub
+        xi[lo] = lb[lo]; xi[hi] = lb[hi]
+        vi[lo | hi] = 0.0
+
+    for g in range(1, maxiter):
+        for i in range(P):
+            th = x[i].copy()
+            match = None
+            for m in range(10):
+                fk, mk, _ = cal_cost2(hand, obs, th, None if m == 0 else match)
+                match = mk
+                sel = min(25, int(math.floor(u01(seed, ST_OPT_PERM, g, i, m) * 26)))
+                xp = th.copy(); xm = th.copy()
+                xp[sel] += 1e-5; xm[sel] -= 1e-5
+                gr = np.zeros(26)
+                gr[sel] = (cal_cost2(hand, obs, xp, match)[0] -
+                           cal_cost2(hand, obs, xm, match)[0]) / (2 * 1e-5)
+                tk = _goldstein(hand, obs, th, gr, match, fk)
+                th = th - tk * gr
+                f2, mk, _ = cal_cost2(hand, obs, th, None if m == 0 else match)
+                match = mk
+                if f2 < pc[i]:
+                    pc[i] = f2; pb[i] = th.copy()
+            clamp(th, v[i])
+            x[i] = th
+        fid = int(np.argmin(pc))
+        if pc[fid] < gcost:
+            gpos, gcost = x[fid].copy(), pc[fid]
+        for i in range(P):
+            for d in range(26):
+                rp = u01(seed, ST_OPT_RP, g, i, d)
+                rg = u01(seed, ST_OPT_RG, g, i, d)
+                v[i, d] = (w * v[i, d] + (c1 * rp) * (pb[i, d] - x[i, d])) + \
+                    (c2 * rg) * (gpos[d] - x[i, d])
+            x[i] = x[i] + v[i]
+            clamp(x[i], v[i])
+        for i in range(P):
+            f = cal_cost(hand, obs, x[i])
+            if f < pc[i]:
+                pc[i] = f; pb[i] = x[i].copy()
+        fid = int(np.argmin(pc))
+        if pc[fid] < gcost:
+            gpos, gcost = x[fid].copy(), pc[fid]
         trace.append(gcost)
     return gpos, gcost, trace
 

@@ -62,9 +62,29 @@ def main():
     np.savez_compressed(HERE / "pso.npz", x0=x0, P=8, maxiter=4, bestp=bestp,
                         bestcost=bestcost, trace=np.array(trace), refined=refined,
                         normals=oracle_np.normals(1000, 4), u01=u)
+    make_optimise(hand, obs_ds)
     for f in sorted(HERE.glob("*.npz")):
         print(f.name, f.stat().st_size)
 
 
+def make_optimise(hand=None, obs=None):
+    """pso_optimise (PSO.cpp:539-712) on the golden frame: 8 particles, maxiter 4,
+    set_pso_params' w, c1, c2 of test_full (testmodel.cpp:101-111)."""
+    if hand is None:
+        geo, rad = hand_data.geometry_cm()
+        hand = oracle_np.Hand(geo, rad)
+        f = np.load(HERE / "frame.npz")
+        obs = oracle_np.Obs(f["depth_cm"], f["dt"], f["cloud"], float(f["scale"]))
+    ub, lb, sd = oracle_np.reference_bounds()
+    x0 = oracle_np.X0.copy()
+    w, c1, c2 = 0.7298, 1.49618, 1.49618
+    bestp, bestcost, trace = oracle_np.pso_optimise(hand, obs, x0, 8, 4, lb, ub, sd, w, c1, c2)
+    np.savez_compressed(HERE / "optimise.npz", x0=x0, P=8, maxiter=4, w=w, c1=c1, c2=c2,
+                        bestp=bestp, bestcost=bestcost, trace=np.array(trace))
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["optimise"]:
+        make_optimise()
+    else:
+        main()

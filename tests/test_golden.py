@@ -74,6 +74,21 @@ def test_pso_refine_golden(oracle, ora_hand, frame):
     np.testing.assert_allclose(x, g["refined"], rtol=0, atol=1e-7)
 
 
+def test_pso_optimise_golden(oracle, ora_hand, frame):
+    """pso_optimise (PSO.cpp:539-712).  Each descent step's central difference (eps 1e-5)
+    amplifies last-ulp cost differences between the two restatements; over 30 descent
+    steps per particle they reach ~2e-7 in the pose, 2e-9 in the cost."""
+    f, obs = frame
+    g = _load("optimise.npz")
+    ub, lb, sd = oracle_np.reference_bounds()
+    bp, bc, tr = oracle.pso_optimise(ora_hand, obs, g["x0"], int(g["P"]), int(g["maxiter"]),
+                                     lb, ub, sd, float(g["w"]), float(g["c1"]),
+                                     float(g["c2"]), seed=1000)
+    np.testing.assert_allclose(bp, g["bestp"], rtol=0, atol=1e-6)
+    assert abs(bc - g["bestcost"]) <= 1e-8 * abs(g["bestcost"])
+    np.testing.assert_allclose(tr, g["trace"], rtol=1e-8)
+
+
 def test_draws_golden(oracle):
     g = _load("pso.npz")
     u = [oracle.u01(1000, s, gg, i, k) for s in (1, 2, 3, 4) for gg in (0, 1, 7)
