@@ -563,4 +563,3 @@ __device__ __forceinline__ double philox_u01(uint64_t seed, uint32_t stream, uin
     return (double)u53 * 0x1.0p-53;
 }
 
-enum { ST_NORMAL = 1, ST_RP = 2, ST_RG = 3, ST_LINK = 4 };

@@ -180,11 +180,11 @@ double host_u01(uint64_t seed, uint32_t stream, uint32_t gen, uint32_t idx, uint
     return (double)((((uint64_t)a) << 21) | (b >> 11)) * 0x1.0p-53;
 }
 
-void make_normals(uint64_t seed, int P, double *out) {
+void make_normals(uint64_t seed, int P, double *out, uint32_t stream) {
     for (int i = 0; i < P; ++i)
         for (int q = 0; q < HPE_DOF / 2; ++q) {
-            const double u1 = host_u01(seed, ST_NORMAL, 0, i, 2 * q);
-            const double u2 = host_u01(seed, ST_NORMAL, 0, i, 2 * q + 1);
+            const double u1 = host_u01(seed, stream, 0, i, 2 * q);
+            const double u2 = host_u01(seed, stream, 0, i, 2 * q + 1);
             const double r = std::sqrt(-2.0 * std::log(1.0 - u1));
             const double t = 6.283185307179586231995926937088370323181152343750 * u2;
             out[HPE_DOF * i + 2 * q] = r * std::cos(t);

@@ -10,12 +10,11 @@
 #include "hpe_layout.hpp"
 
 namespace hpe {
-enum { ST_NORMAL = 1, ST_RP = 2, ST_RG = 3, ST_LINK = 4 };
 void build_dev_hand(const hpe_hand_params &p, DevHand &h);
 int preprocess_depth(const float *depth_mm, int to_cm, int downsample, double focal,
                      double *depth_cm, float *dt, double *cloud, int32_t *n_out,
                      double *scale_out, double *dtmax_out, double K[9]);
 double host_u01(uint64_t seed, uint32_t stream, uint32_t gen, uint32_t idx, uint32_t k);
-void make_normals(uint64_t seed, int P, double *out);
+void make_normals(uint64_t seed, int P, double *out, uint32_t stream = ST_NORMAL);
 int make_links(uint64_t seed, int P, int G, std::vector<int> &outl);
 }  // namespace hpe

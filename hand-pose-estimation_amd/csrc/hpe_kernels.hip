@@ -646,6 +646,72 @@ __device__ __forceinline__ void gold_down(double a, double &b, double &alpha) {
     alpha = 0.5 * (a + alpha);
 }
 
+// goldstein(x, g, matchId, f_k, optfunc, tk, 30) (PSO.cpp:438-480) along rs.p from rs.x0
+// with frozen correspondences, speculated RF_DEPTH levels per round: wave w evaluates tree
+// node w + 1 (root = current alpha, child 2n = "f1 > armijo" branch, 2n + 1 = "f1 <
+// goldstein" branch) and the walk replays the serial rules.  Returns tk (0 after 30
+// rejected trials); the accepted node's spheres are copied into rs.base and its cost to
+// *f_acc.  evals grows by the serial evaluation count.
+__device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const CloudView &cv,
+                                            const DevHand *__restrict__ H,
+                                            const int32_t *__restrict__ match, double fk,
+                                            double gp, int &evals, double *f_acc) {
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    double A = 0, B = 1e100, alpha = 0.5, tk = 0;
+    int it = 0, accepted = -1;
+    bool done = false;
+    while (!done) {
+        if (w < (1 << RF_DEPTH) - 1) {
+            const int node = w + 1, depth = 31 - __builtin_clz(node);
+            double a = A, b = B, al2 = alpha;
+            for (int k = depth - 1; k >= 0; --k) {
+                if ((node >> k) & 1) gold_up(a, b, al2);
+                else gold_down(a, b, al2);
+            }
+            if (l < HPE_DOF) rs.w[w].th[l] = rs.x0[l] + al2 * rs.p[l];
+            wave_sync();
+            const double f = eval_wave_frozen(rs.w[w], o, cv, H, match);
+            if (l == 0) rs.f[w] = f;
+        }
+        __syncthreads();
+        int node = 1;
+        accepted = -1;
+        for (int lev = 0; lev < RF_DEPTH && !done; ++lev) {
+            if (it >= 30) {
+                done = true;
+                tk = 0;
+                break;
+            }
+            ++it;
+            const double f1 = rs.f[node - 1];
+            const double armijo = fk + 0.25 * alpha * gp;
+            const double gold = fk + (1 - 0.25) * alpha * gp;
+            if (f1 <= armijo) {
+                if (f1 >= gold) {
+                    tk = alpha;
+                    done = true;
+                    accepted = node - 1;
+                } else {
+                    gold_up(A, B, alpha);
+                    node = 2 * node + 1;
+                }
+            } else {
+                gold_down(A, B, alpha);
+                node = 2 * node;
+            }
+        }
+        if (!done && it >= 30) done = true;  // tk stays 0
+        if (done && accepted >= 0) {  // keep the accepted node's spheres for the next f_k
+            for (int q = t; q < (int)(offsetof(FkSm, J) / 8); q += RF_NT)
+                ((double *)&rs.base)[q] = ((const double *)&rs.w[accepted])[q];
+            if (f_acc) *f_acc = rs.f[accepted];
+        }
+        __syncthreads();
+    }
+    evals += it;
+    return tk;
+}
+
 // Grid 1 or 1 + PREP_WG: workgroup 0 refines the selected frame (do_refine != 0); the
 // others, when present, prepare the NEXT frame meanwhile (hpe_prep.hpp) on
 // CUs this single-workgroup refine leaves idle -- one launch, one stream, no cross-queue
@@ -742,57 +808,7 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
             }
             const double gp = v1 + v2;
             // goldstein(x0, grad, matchId, f_k, optfunc, tk, 30)
-            double A = 0, B = 1e100, alpha = 0.5, tk = 0;
-            int it = 0, accepted = -1;
-            bool done = false;
-            while (!done) {
-                if (w < (1 << RF_DEPTH) - 1) {
-                    const int node = w + 1, depth = 31 - __builtin_clz(node);
-                    double a = A, b = B, al2 = alpha;
-                    for (int k = depth - 1; k >= 0; --k) {
-                        if ((node >> k) & 1) gold_up(a, b, al2);
-                        else gold_down(a, b, al2);
-                    }
-                    if (l < HPE_DOF) rs.w[w].th[l] = rs.x0[l] + al2 * rs.p[l];
-                    wave_sync();
-                    const double f = eval_wave_frozen(rs.w[w], o, cv, H, match);
-                    if (l == 0) rs.f[w] = f;
-                }
-                __syncthreads();
-                int node = 1;
-                accepted = -1;
-                for (int lev = 0; lev < RF_DEPTH && !done; ++lev) {
-                    if (it >= 30) {
-                        done = true;
-                        tk = 0;
-                        break;
-                    }
-                    ++it;
-                    const double f1 = rs.f[node - 1];
-                    const double armijo = fk + 0.25 * alpha * gp;
-                    const double gold = fk + (1 - 0.25) * alpha * gp;
-                    if (f1 <= armijo) {
-                        if (f1 >= gold) {
-                            tk = alpha;
-                            done = true;
-                            accepted = node - 1;
-                        } else {
-                            gold_up(A, B, alpha);
-                            node = 2 * node + 1;
-                        }
-                    } else {
-                        gold_down(A, B, alpha);
-                        node = 2 * node;
-                    }
-                }
-                if (!done && it >= 30) done = true;  // tk stays 0
-                if (done && accepted >= 0) {  // keep the accepted node's spheres for f_k
-                    for (int q = t; q < (int)(offsetof(FkSm, J) / 8); q += RF_NT)
-                        ((double *)&rs.base)[q] = ((const double *)&rs.w[accepted])[q];
-                }
-                __syncthreads();
-            }
-            evals += it;
+            const double tk = gold_tree(rs, o, cv, H, match, fk, gp, evals, nullptr);
             sc.lap(22);
             if (tk == 0) cnt += 1;
             {  // tol = sqrt(sum(grad % grad)): arrayops::accumulate over the squares
@@ -814,6 +830,8 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
     if (t < HPE_DOF) x0g[t] = rs.x0[t];
     if (t == 0 && evals_out) *evals_out = evals;
 }
+
+#include "hpe_optimise.hpp"
 
 // ------------------------------------------------------------------ synthetic frames
 __global__ void k_render(const double *__restrict__ S, const DevHand *__restrict__ H,

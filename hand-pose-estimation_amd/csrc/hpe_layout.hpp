@@ -11,6 +11,11 @@
 #define HPE_IMG_H 240
 #define HPE_IMG_W 320
 
+// Philox4x32-10 streams (counter = {k/2, particle, generation, stream}): pso_evolve uses
+// 1..4, pso_optimise 5..8.
+enum { ST_NORMAL = 1, ST_RP = 2, ST_RG = 3, ST_LINK = 4, ST_OPT_PERM = 5, ST_OPT_RP = 6,
+       ST_OPT_RG = 7, ST_OPT_NORMAL = 8 };
+
 // Hand constants, one copy per context in HBM (read with scalar loads).
 struct DevHand {
     double Fc[5], Fs[5], FLc[5], FLs[5];  // T01 / Trf: cos, sin, L*cos, L*sin
@@ -67,3 +72,21 @@ struct DevSwarm {
     int P, G, K;
 };
 
+
+// pso_optimise state (PSO.cpp:539-712): global-best PSO whose particles first take ten
+// single-coordinate Goldstein steps each generation.  The gbest position is needed by the
+// velocity update inside the generation, so it is resolved at the end of every phase by
+// the last workgroup to arrive (gbest[26] = cost, gbest[27] = count).
+struct DevOpt {
+    double *x, *v, *pb;       // P x 26
+    double *pc;               // P  pbest costs
+    double *gbest;            // 28: position, cost, count
+    double *trace;            // [G] gbest cost after each generation
+    int32_t *match;           // P x n_cap correspondences (clouds too large for LDS)
+    unsigned *ctr;            // arrival counter (reset by the last workgroup)
+    const double *normals;    // P x 26 (stream ST_OPT_NORMAL)
+    const double *bounds;     // lb[26], ub[26], std[26]
+    uint64_t seed;
+    int P, G, n_cap;
+    double w, c1, c2;
+};

@@ -472,6 +472,17 @@ int PSO::pso_evolve(costfunc &optfunc, arma::vec &x0, int num_particles, arma::v
     return 1;
 }
 
+int PSO::pso_optimise(costfunc &optfunc, arma::vec &x0, int num_p, arma::vec &bestp) {
+    // PSO.cpp:539-712
+    if (x0.n_elem != 26) throw std::invalid_argument("x0 must have 26 elements");
+    hpe_ctx *c = optfunc.sync();
+    push(c);
+    bestp.zeros(26);
+    check(c, hpe_pso_optimise(c, x0.memptr(), num_p, bestp.memptr(), &gbest_cost_, nullptr, 0),
+          "hpe_pso_optimise");
+    return 1;
+}
+
 double PSO::track_frame(costfunc &optfunc, arma::vec &x0, int num_particles, bool refine) {
     if (x0.n_elem != 26) throw std::invalid_argument("x0 must have 26 elements");
     hpe_ctx *c = optfunc.sync();

@@ -154,12 +154,15 @@ private:
     arma::uvec matchIdx;
 };
 
-// PSO.h:15-72 (the pso_solve / pso_optimise variants are listed in DESIGN.md §8)
+// PSO.h:15-72 (the pso_solve variant is listed in DESIGN.md §8)
 class PSO {
 public:
     PSO();
     void refine_init_pose(arma::vec &x0, costfunc &optfunc);
     int pso_evolve(costfunc &optfunc, arma::vec &x0, int num_particles, arma::vec &bestp);
+    // PSO.cpp:539-712: descent + global-best PSO (omega / phip / phig); the reference
+    // marks it "merely used for testing gradient descent + pso"
+    int pso_optimise(costfunc &optfunc, arma::vec &x0, int num_p, arma::vec &bestp);
     void set_pso_params(arma::vec &upperbound, arma::vec &lowerbound, arma::vec &std,
                         double &omega, double &phip, double &phig, int &maxiter,
                         double &minstep, double &minfunc);

@@ -383,6 +383,25 @@ class PSO:
         self.last_gbest_cost = bc.value
         return 1
 
+    def pso_optimise(self, optfunc: costfunc, x0, num_p, bestp):
+        """PSO.cpp:539-712 (descent + global-best PSO with omega / phip / phig of
+        set_pso_params): bestp (26,) filled in place; returns 1.  The gbest cost after each
+        generation is kept in last_optimise_trace."""
+        ctx = optfunc.ctx
+        optfunc._sync_frame()
+        self._push(ctx)
+        x = _lib.as_f64(x0, (26,))
+        out = np.zeros(26); bc = C.c_double(0)
+        G = max(self.maxiter - 1, 0)
+        tr = np.zeros(max(G, 1))
+        ctx.check(ctx.lib.hpe_pso_optimise(ctx.h, ptr(x, C.c_double), int(num_p),
+                                           ptr(out, C.c_double), C.byref(bc),
+                                           ptr(tr, C.c_double), G))
+        bestp[...] = out
+        self.last_gbest_cost = bc.value
+        self.last_optimise_trace = tr[:G]
+        return 1
+
     def trace(self, optfunc: costfunc):
         G = self.maxiter - 1
         g = np.zeros(max(G, 1)); cnt = np.zeros(max(G, 1), dtype=np.int32)

@@ -136,8 +136,9 @@ int hpe_cal_cost2(hpe_ctx *ctx, const double theta[26], int32_t *match_inout,
 int hpe_eval_spheres(hpe_ctx *ctx, const double *S, int P, int compute_corr,
                      int32_t *match_inout, double *terms_out);
 
-/* PSO::set_pso_params (PSO.cpp:38-54).  omega/phip/phig/minstep/minfunc are kept
- * for API parity; pso_evolve uses the SPSO-2011 constants (PSO.cpp:772-774). */
+/* PSO::set_pso_params (PSO.cpp:38-54).  pso_evolve uses the SPSO-2011 constants
+ * (PSO.cpp:772-774); pso_optimise uses omega/phip/phig; minstep/minfunc are kept for
+ * API parity (no caller reads them). */
 int hpe_set_pso_params(hpe_ctx *ctx, const double ub[26], const double lb[26],
                        const double stdv[26], double omega, double phip, double phig,
                        int maxiter, double minstep, double minfunc);
@@ -152,6 +153,14 @@ int hpe_pso_evolve(hpe_ctx *ctx, const double x0[26], int num_p, double bestp[26
 /* Per-generation trace of the last pso_evolve (debug / parity):
  * gbest cost, stagnation count, topology generation; arrays of maxiter-1. */
 int hpe_pso_trace(hpe_ctx *ctx, double *gbest, int32_t *count, int32_t *topo, int n);
+
+/* PSO::pso_optimise(optfunc, x0, num_p, bestp) (PSO.cpp:539-712): global-best PSO with
+ * omega/phip/phig whose particles first take 10 single-coordinate Goldstein steps every
+ * generation.  maxiter-1 generations.  Draws: Philox streams 5..8 under hpe_set_seed's
+ * seed (the reference draws from an unseeded Armadillo stream).  bestcost_out optional;
+ * gbest_trace optional, trace_len <= maxiter-1 gbest costs, one per generation. */
+int hpe_pso_optimise(hpe_ctx *ctx, const double x0[26], int num_p, double bestp[26],
+                     double *bestcost_out, double *gbest_trace, int trace_len);
 
 /* PSO::refine_init_pose(x0, optfunc) (PSO.cpp:216-266).  evals_out optional. */
 int hpe_refine_init_pose(hpe_ctx *ctx, double x0[26], int32_t *evals_out);
@@ -191,7 +200,9 @@ int hpe_track_pipelined(hpe_ctx *ctx, int num_p, int refine, double *d_state,
 #define HPE_PROF_PSO_INIT 2  /* k_pso_init */
 #define HPE_PROF_PSO_FINAL 3 /* k_pso_final */
 #define HPE_PROF_PREP 4      /* k_preprocess (hpe_prepare_frame, preprocessing stream) */
-#define HPE_PROF_KERNELS 5
+#define HPE_PROF_OPT_DESCENT 5 /* k_opt_descent: pso_optimise descent phase */
+#define HPE_PROF_OPT_MOVE 6    /* k_opt_move: pso_optimise velocity / cost phase */
+#define HPE_PROF_KERNELS 7
 int hpe_profile_enable(hpe_ctx *ctx, int on);
 int hpe_profile_read(hpe_ctx *ctx, int32_t *launches, double *total_ms, double *min_ms,
                      double *max_ms);

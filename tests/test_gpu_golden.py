@@ -68,3 +68,20 @@ def test_pso_refine_golden_gpu(setup):
     x = g["x0"].copy()
     pso.refine_init_pose(x, cf)
     np.testing.assert_allclose(x, g["refined"], rtol=0, atol=1e-6)
+
+
+def test_pso_optimise_golden_gpu(setup):
+    """pso_optimise against the numpy restatement's fixture (tolerances as in
+    test_gpu_parity.test_pso_optimise)."""
+    import hpe
+    gh, om, cf, f = setup
+    g = _load("optimise.npz")
+    ub, lb, sd = oracle_np.reference_bounds()
+    pso = hpe.PSO()
+    pso.set_pso_params(ub, lb, sd, float(g["w"]), float(g["c1"]), float(g["c2"]),
+                       int(g["maxiter"]), 1e-8, 1e-8)
+    bp = np.zeros(26)
+    assert pso.pso_optimise(cf, g["x0"], int(g["P"]), bp) == 1
+    np.testing.assert_allclose(bp, g["bestp"], rtol=0, atol=1e-5)
+    assert abs(pso.last_gbest_cost - g["bestcost"]) <= 1e-7 * abs(g["bestcost"])
+    np.testing.assert_allclose(pso.last_optimise_trace, g["trace"], rtol=1e-7)

@@ -183,6 +183,37 @@ def test_pso_evolve(oracle, ora_hand, gpu_hand, np_hand, P, maxiter):
         assert np.array_equal(topo, tr["topo"])
 
 
+@pytest.mark.parametrize("P,maxiter,downsample", [(16, 4, True), (5, 3, True), (1, 2, True),
+                                                  (4, 2, False)])
+def test_pso_optimise(oracle, ora_hand, gpu_hand, np_hand, P, maxiter, downsample):
+    """pso_optimise (PSO.cpp:539-712).  Every descent step differentiates the cost with
+    eps 1e-5, so last-ulp cost differences (tree vs 2-accumulator sums) grow to ~1e-7 in
+    the pose over a generation's 10 steps: bestp |diff| <= 1e-5, costs relative 1e-7.
+    downsample=False: a full-resolution cloud (> 2048 points), matchId in HBM."""
+    import hpe
+    truth = hand_data.trajectory(2, seed=21)[1]
+    d = oracle_np.render_depth_mm(np_hand, truth)
+    obs, om = _obs_pair(oracle, gpu_hand, d, downsample=downsample)
+    assert (obs.n > 2048) == (not downsample)
+    cf = hpe.costfunc(gpu_hand, om)
+    ub, lb, sd = oracle_np.reference_bounds()
+    w, c1, c2 = 0.7298, 1.49618, 1.49618
+    pso = hpe.PSO()
+    pso.set_pso_params(ub, lb, sd, w, c1, c2, maxiter, 1e-8, 1e-8)
+    bestp = np.zeros(26)
+    x0 = oracle_np.X0.copy()
+    assert pso.pso_optimise(cf, x0, P, bestp) == 1
+    rb, rc, tr = oracle.pso_optimise(ora_hand, obs, x0, P, maxiter, lb, ub, sd, w, c1, c2,
+                                     seed=1000)
+    print("pso_optimise P=%d maxiter=%d: |dbestp| %.3g, dcost %.3g" %
+          (P, maxiter, np.abs(bestp - rb).max(), abs(pso.last_gbest_cost - rc) / abs(rc)))
+    np.testing.assert_allclose(bestp, rb, rtol=0, atol=1e-5)
+    assert abs(pso.last_gbest_cost - rc) <= 1e-7 * abs(rc)
+    np.testing.assert_allclose(pso.last_optimise_trace, tr, rtol=1e-7)
+    # the descent lowers the cost below pso_evolve-free initialisation
+    assert tr[-1] <= tr[0]
+
+
 def test_refine_init_pose(oracle, ora_hand, gpu_hand, np_hand):
     import hpe
     truth = hand_data.trajectory(2, seed=4)[1]
