@@ -657,6 +657,8 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
                                             const int32_t *__restrict__ match, double fk,
                                             double gp, int &evals, double *f_acc) {
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    StampClock sc;
+    sc.start();
     double A = 0, B = 1e100, alpha = 0.5, tk = 0;
     int it = 0, accepted = -1;
     bool done = false;
@@ -694,10 +696,12 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
                 } else {
                     gold_up(A, B, alpha);
                     node = 2 * node + 1;
+                    if (HPE_STAMPS && blockIdx.x == 0 && t == 0) hpe_stamps[8] += 1;
                 }
             } else {
                 gold_down(A, B, alpha);
                 node = 2 * node;
+                if (HPE_STAMPS && blockIdx.x == 0 && t == 0) hpe_stamps[7] += 1;
             }
         }
         if (!done && it >= 30) done = true;  // tk stays 0
@@ -707,8 +711,14 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
             if (f_acc) *f_acc = rs.f[accepted];
         }
         __syncthreads();
+        sc.lap(19);  // one speculated round
     }
     evals += it;
+    if (HPE_STAMPS && blockIdx.x == 0 && t == 0) {  // decision statistics (diagnostic build)
+        hpe_stamps[9] += (tk != 0) ? 1 : 0;
+        hpe_stamps[30] += (unsigned long long)it;
+        hpe_stamps[32 + 9] += 1;
+    }
     return tk;
 }
 

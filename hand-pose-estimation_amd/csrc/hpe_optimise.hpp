@@ -124,6 +124,8 @@ __global__ __launch_bounds__(RF_NT) void k_opt_descent(DevOpt op, const DevObs *
     const double e5 = 1e-5;  // cal_gradient eps (PSO.cpp:384)
     double fk = 0;
     int evals = 0;
+    StampClock sc;
+    sc.start();
     for (int m = 0; m < OPT_GRADITER; ++m) {
         if (m == 0) {  // f_k = cal_cost2(ctheta, matchId, true)
             if (t < HPE_DOF) rs.base.th[t] = rs.x0[t];
@@ -135,6 +137,7 @@ __global__ __launch_bounds__(RF_NT) void k_opt_descent(DevOpt op, const DevObs *
             double co = (t < 144) ? collide_term(rs.base, t, H) : 0.0;
             block_sum3<RF_NT>(rs.red, al, dep, co);
             fk = (al * o.lambda + dep) + co;
+            sc.lap(26);
         }
         const int sel = sel_s[m];
         if (w < 2) {  // cal_gradient: theta +/- eps on coordinate sel, frozen matchId
@@ -157,8 +160,10 @@ __global__ __launch_bounds__(RF_NT) void k_opt_descent(DevOpt op, const DevObs *
             v2 += rs.g[b] * rs.p[b];
         }
         const double gp = v1 + v2;
+        sc.lap(27);
         double facc = fk;
         const double tk = gold_tree(rs, o, cv, H, match, fk, gp, evals, &facc);
+        sc.start();
         if (t < HPE_DOF) rs.x0[t] = rs.x0[t] - tk * rs.g[t];
         __syncthreads();
         double f2 = fk;  // tk == 0: theta unchanged, same matchId -> same cost
@@ -179,6 +184,7 @@ __global__ __launch_bounds__(RF_NT) void k_opt_descent(DevOpt op, const DevObs *
             if (t < HPE_DOF) pbrow[t] = rs.x0[t];
         }
         fk = f2;
+        sc.lap(28);
     }
     if (t < HPE_DOF) {  // check_constraints(ctheta, cveloc): above max -> MIN (:372)
         const double *lb = op.bounds, *ub = op.bounds + HPE_DOF;

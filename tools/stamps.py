@@ -37,7 +37,8 @@ names = {4: "gen: prologue (og + hand)", 5: "gen: block-0 span (cycles)",
          16: "wave: align frozen", 17: "wave: collision", 18: "wave: 3 reductions",
          20: "refine: corr eval", 21: "refine: grad evals", 22: "refine: goldstein",
          23: "refine: iter glue", 24: "prep (fused): band workgroups (incl. merge)",
-         25: "prep (fused): DT workgroup"}
+         25: "prep (fused): DT workgroup", 19: "goldstein: speculated round",
+         26: "opt: m=0 corr eval", 27: "opt: grad (2 waves)", 28: "opt: step tail (+m=0 re-match)"}
 tot = np.zeros(64)
 for f in range(1, nfr + 1):
     ctx.select_frame(f)
@@ -61,3 +62,21 @@ for k, nm in names.items():
     n = tot[32 + k]
     if n:
         print(f"{nm:34s} laps {int(n):7d}  avg {tot[k] / n:10.1f} cyc  total/frame {tot[k] / nfr:12.0f} cyc")
+
+# pso_optimise (test_full settings, P = 32): descent-phase breakdown of block 0
+ctx.select_frame(1)
+lib.hpe_debug_stamps(st.ctypes.data_as(C.POINTER(C.c_uint64)))  # reset
+x = np.ascontiguousarray(poses[0]); bp = np.zeros(26); bc = C.c_double(0)
+ctx.check(lib.hpe_set_pso_params(ctx.h, _lib.ptr(ub, C.c_double), _lib.ptr(lb, C.c_double),
+                                 _lib.ptr(sd, C.c_double), 0.7298, 1.49618, 1.49618, 21, 1e-8,
+                                 1e-8))
+ctx.check(lib.hpe_pso_optimise(ctx.h, _lib.ptr(x, C.c_double), 32, _lib.ptr(bp, C.c_double),
+                               C.byref(bc), None, 0))
+lib.hpe_debug_stamps(st.ctypes.data_as(C.POINTER(C.c_uint64)))
+print("pso_optimise P=32 maxiter=21 (20 descent launches, block 0):")
+print("  goldstein searches %d: accepted %d, trials %d, down %d, up %d" %
+      (st[32 + 9], st[9], st[30], st[7], st[8]))
+for k in (26, 27, 19, 28, 15, 16, 17, 18):
+    n = st[32 + k]
+    if n:
+        print(f"{names[k]:34s} laps {int(n):7d}  avg {st[k] / n:10.1f} cyc  per launch {st[k] / 20:12.0f} cyc")
