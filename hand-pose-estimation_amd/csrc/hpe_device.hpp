@@ -27,6 +27,10 @@
 #define HPE_STAMPS 0
 #endif
 __device__ unsigned long long hpe_stamps[64];
+#if HPE_STAMPS
+#define HPE_GOLD_LOG 65536
+__device__ unsigned long long hpe_gold_log[1 + HPE_GOLD_LOG];  // [0] = count
+#endif
 struct StampClock {
     unsigned long long t, t0 = 0, r0 = 0;
     // whole-kernel span of block 0: shader cycles into slot k, 100 MHz ticks into k + 1

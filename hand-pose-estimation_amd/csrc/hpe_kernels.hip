@@ -662,6 +662,7 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
     double A = 0, B = 1e100, alpha = 0.5, tk = 0;
     int it = 0, accepted = -1;
     bool done = false;
+    [[maybe_unused]] unsigned long long path = 0;  // diagnostic build: decision bits (1 = up)
     while (!done) {
         if (w < (1 << RF_DEPTH) - 1) {
             const int node = w + 1, depth = 31 - __builtin_clz(node);
@@ -696,6 +697,7 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
                 } else {
                     gold_up(A, B, alpha);
                     node = 2 * node + 1;
+                    if (HPE_STAMPS) path |= 1ull << (it - 1);
                     if (HPE_STAMPS && blockIdx.x == 0 && t == 0) hpe_stamps[8] += 1;
                 }
             } else {
@@ -719,6 +721,14 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
         hpe_stamps[30] += (unsigned long long)it;
         hpe_stamps[32 + 9] += 1;
     }
+#if HPE_STAMPS
+    if (t == 0) {  // every search of every block: {path bits, trials << 32, accepted << 40}
+        const unsigned long long k = atomicAdd(&hpe_gold_log[0], 1ull);
+        if (k < HPE_GOLD_LOG)
+            hpe_gold_log[1 + k] = path | ((unsigned long long)it << 32) |
+                                  ((unsigned long long)(tk != 0) << 40);
+    }
+#endif
     return tk;
 }
 
@@ -873,6 +883,21 @@ __global__ void k_render(const double *__restrict__ S, const DevHand *__restrict
     }
     out[pix] = (best < __builtin_inf()) ? (float)(best * 10.0) : 0.0f;
 }
+
+#if HPE_STAMPS
+// Diagnostic build only: the Goldstein decision log (not part of include/hpe.h).
+extern "C" int hpe_debug_gold_log(unsigned long long *out, int n) {
+    if (!out || n < 1) return HPE_E_ARG;
+    if (n > HPE_GOLD_LOG + 1) n = HPE_GOLD_LOG + 1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hpe_gold_log), sizeof(unsigned long long) * n, 0,
+                            hipMemcpyDeviceToHost) != hipSuccess)
+        return HPE_E_HIP;
+    const unsigned long long z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(hpe_gold_log), &z, sizeof(z), 0, hipMemcpyHostToDevice) != hipSuccess)
+        return HPE_E_HIP;
+    return HPE_OK;
+}
+#endif
 
 extern "C" int hpe_debug_stamps(unsigned long long *out64) {
     if (!out64) return HPE_E_ARG;

@@ -80,7 +80,9 @@ def load(path: os.PathLike | str | None = None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = Path(path) if path else LIB_PATH
+    # HPE_LIB_VARIANT=<file in the package dir>: A/B a second in-tree build (tools only)
+    variant = os.environ.get("HPE_LIB_VARIANT")
+    p = Path(path) if path else (PKG_DIR / variant if variant else LIB_PATH)
     if not p.exists():
         raise RuntimeError(f"{p} not built: run `make -C {PKG_DIR}` (no CPU fallback exists)")
     lib = C.CDLL(str(p))
