@@ -2,10 +2,12 @@
 """bench.py -- particle-evals/s + tracked FPS of the MI355X PSO hand tracker.
 
 Workload (BASELINE.json configs[1]/[2]): a step is ONE TRACKED FRAME of a synthetic
-240x320 depth sequence -- refine_init_pose, pso_evolve with 256 particles x 30
-generations (reference maxiter = 31), cal_cost(bestp), x0 <- bestp -- exactly the body
-of test_full (testmodel.cpp:124-138), on frames already preprocessed and resident in
-HBM.  N = 250 cloud points (the reference's downsample=true default).
+240x320 depth sequence -- next_frame preprocessing of the raw float32 mm depth (on the
+GPU, inside the previous frame's refine launch), refine_init_pose, pso_evolve with 256
+particles x 30 generations (reference maxiter = 31), cal_cost(bestp), x0 <- bestp --
+the body of test_full's loop (testmodel.cpp:117-139).  The raw frames sit in host
+memory, as load_data reads them; --resident prepares them all in HBM first.
+N = 250 cloud points (the reference's downsample=true default; --full-cloud: all).
 
   value        = PSO particle evaluations per second over all ranks
                  (P*(G+1) per frame per rank; refine and final evaluations are not counted)
@@ -97,11 +99,33 @@ def cpu_baseline(args, sizes_hint):
         el = time.perf_counter() - t0
         if el >= args.cpu_seconds or done >= 4096:
             break
-    return {"value": P * (G + 1) * done / el, "unit": "particle-evals/s", "cores": threads,
-            "kind": "port", "tracked_fps": done / el,
-            "sample": f"{done} tracked frames incl. preprocessing ({P}p x {G} gen, N={n_pts}, "
-                      f"refine={'off' if args.no_refine else 'on'}) of the same synthetic "
-                      f"sequence in {el:.1f} s, oracle/hpe_oracle.c with {threads} OpenMP threads"}
+    out = {"value": P * (G + 1) * done / el, "unit": "particle-evals/s", "cores": threads,
+           "kind": "port", "tracked_fps": done / el,
+           "sample": f"{done} tracked frames incl. preprocessing ({P}p x {G} gen, N={n_pts}, "
+                     f"refine={'off' if args.no_refine else 'on'}) of the same synthetic "
+                     f"sequence in {el:.1f} s, oracle/hpe_oracle.c with {threads} OpenMP threads"}
+    # the single-thread rate of the same loop, a shorter sample
+    x, done1, t0 = poses[0].copy(), 0, time.perf_counter()
+    while True:
+        obs = o.preprocess(raw[done1 % len(raw)], downsample=not args.full_cloud)
+        if not args.no_refine:
+            x, _ = o.refine(h, obs, x)
+        x, _, _ = o.pso_evolve(h, obs, x, P, G + 1, lb, ub, sd, seed=1000, nthreads=1)
+        o.cal_cost(h, obs, x)
+        done1 += 1
+        el1 = time.perf_counter() - t0
+        if el1 >= args.cpu_seconds / 3 or done1 >= 1024:
+            break
+    out["one_thread"] = {"value": P * (G + 1) * done1 / el1, "tracked_fps": done1 / el1,
+                         "sample": f"{done1} tracked frames in {el1:.1f} s, 1 thread"}
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                out["cpu_model"] = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return out
 
 
 def load_pmc(P, n_points):

@@ -112,71 +112,103 @@ __device__ __forceinline__ double deg2rad(double a) {
 //          cur = T00*Tgb*F*(A*B)*C3*C4 with no exchange; the 9 entries of A*B it needs
 //          (T12*T23 / T01*T12) are independent of the chain and overlap with it.  The
 //          lane then writes coordinate r of its digit's spheres.
-__device__ __forceinline__ void fk_wave(FkSm &f, const DevHand *__restrict__ H) {
+// The global position u = theta[3..5] enters every joint translation only as the
+// innermost addend (T00 is a pure translation, fingermodel.cpp:157-160, 289):
+//   J1 = X1 + u,  J0 = X0 + J1,  J2 = X2 + J1,  J3 = X3 + J2,  J4 = X4 + J3
+// with X0..X4 depending on the rotations and digit angles only.  FK_STORE_X keeps them;
+// FK_TRANSLATE rebuilds the joints of a theta that differs from the stored one only in
+// u with those five adds -- the same operations in the same order, so bit-identical.
+enum FkMode { FK_FULL = 0, FK_STORE_X = 1, FK_TRANSLATE = 2 };
+struct FkX {
+    double x[15][5];
+};
+
+template <int MODE>
+__device__ __forceinline__ void fk_wave_t(FkSm &f, const DevHand *__restrict__ H, FkX *X) {
     const int l = threadIdx.x & 63;
     StampClock sc;
     sc.start();
-    if (l < 23) {
-        double a;
-        if (l == 0) a = deg2rad(f.th[0] + 180);  // TWS, fingermodel.cpp:91
-        else if (l < 3) a = deg2rad(f.th[l]);    // ANG, ROT
-        else a = deg2rad(f.th[6 + (l - 3)]);     // digit angles, handmodel.cpp:141-146
-        double s, c;
-        sincos(a, &s, &c);
-        f.sn[l] = s;
-        f.cs[l] = c;
+    if (MODE != FK_TRANSLATE) {
+        if (l < 23) {
+            double a;
+            if (l == 0) a = deg2rad(f.th[0] + 180);  // TWS, fingermodel.cpp:91
+            else if (l < 3) a = deg2rad(f.th[l]);    // ANG, ROT
+            else a = deg2rad(f.th[6 + (l - 3)]);     // digit angles, handmodel.cpp:141-146
+            double s, c;
+            sincos(a, &s, &c);
+            f.sn[l] = s;
+            f.cs[l] = c;
+        }
+        wave_sync();
     }
-    wave_sync();
     sc.lap(13);
     if (l < 15) {
         const int d = l / 3, r = l - 3 * (l / 3);
-        const double c1 = f.cs[3 + 4 * d], s1 = f.sn[3 + 4 * d];
-        const double c2 = f.cs[4 + 4 * d], s2 = f.sn[4 + 4 * d];
-        const double c3 = f.cs[5 + 4 * d], s3 = f.sn[5 + 4 * d];
-        const double c4 = f.cs[6 + 4 * d], s4 = f.sn[6 + 4 * d];
-        const double L1 = H->L[d][1], L2 = H->L[d][2], L3 = H->L[d][3];
-        const double tc = H->twc[d], ts = H->tws[d];
-        // Columns 0, 1, 3 of A*B with A = [[c1,0,-s1,0],[s1,0,c1,0],[0,-1,0,0]] and
-        // B = [[c2,-s2*tc,s2*ts,L1*c2],[s2,c2*tc,-c2*ts,L1*s2],[0,ts,tc,0]]
-        // (thumbmodel.cpp:144-153; fingers tc = 1, ts = 0, fingermodel.cpp:137-145).
-        // Each entry is the reference's k-ordered sum with its exact-zero terms dropped.
-        const double b01 = -s2 * tc, b11 = c2 * tc, L1c2 = L1 * c2, L1s2 = L1 * s2;
-        const double AB00 = c1 * c2, AB10 = s1 * c2, AB20 = -s2;
-        const double AB01 = c1 * b01 + (-s1) * ts, AB11 = s1 * b01 + c1 * ts, AB21 = -b11;
-        const double AB03 = c1 * L1c2, AB13 = s1 * L1c2, AB23 = -L1s2;
-        const double cz = f.cs[0], sz = f.sn[0], cy = f.cs[1], sy = f.sn[1];
-        const double cxr = f.cs[2], sxr = f.sn[2];
-        double z0, z1, z2;  // row r of Rz
-        if (r == 0) { z0 = cz; z1 = -sz; z2 = 0; }
-        else if (r == 1) { z0 = sz; z1 = cz; z2 = 0; }
-        else { z0 = 0; z1 = 0; z2 = 1; }
-        // (Rz*Ry) row r, Ry = [[cy,0,sy],[0,1,0],[-sy,0,cy]]
-        const double q0 = z0 * cy + z2 * (-sy);
-        const double q1 = z1;
-        const double q2 = z0 * sy + z2 * cy;
-        // Tgb row r = q * Rx, Rx = [[1,0,0],[0,cx,-sx],[0,sx,cx]]; cur0 = T00*Tgb
-        const double g0 = q0;
-        const double g1 = q1 * cxr + q2 * sxr;
-        const double g2 = q1 * (-sxr) + q2 * cxr;
         const double u = f.th[3 + r];
-        // cur1 = cur0 * F  (rotation about z + translation L0)
-        const double h0 = g0 * H->Fc[d] + g1 * H->Fs[d];
-        const double h1 = g0 * (-H->Fs[d]) + g1 * H->Fc[d];
-        const double h2 = g2;
-        const double h3 = (g0 * H->FLc[d] + g1 * H->FLs[d]) + u;
-        const double J1 = h3;
-        const double J0 = (h0 * H->T10x[d] + h1 * H->T10y[d]) + h3;  // (cur*T10) at i == 1
-        // cur2 = cur1 * AB
-        const double k0 = (h0 * AB00 + h1 * AB10) + h2 * AB20;
-        const double k1 = (h0 * AB01 + h1 * AB11) + h2 * AB21;
-        const double k3 = ((h0 * AB03 + h1 * AB13) + h2 * AB23) + h3;
-        const double J2 = k3;
-        // cur3 = cur2 * C3, then the translation of cur3 * C4
-        const double m0 = k0 * c3 + k1 * s3;
-        const double m1 = k0 * (-s3) + k1 * c3;
-        const double m3 = (k0 * (L2 * c3) + k1 * (L2 * s3)) + k3;
-        const double J3 = m3;
-        const double J4 = (m0 * (L3 * c4) + m1 * (L3 * s4)) + m3;
+        double X0, X1, X2, X3, X4;
+        if (MODE == FK_TRANSLATE) {
+            X0 = X->x[l][0];
+            X1 = X->x[l][1];
+            X2 = X->x[l][2];
+            X3 = X->x[l][3];
+            X4 = X->x[l][4];
+        } else {
+            const double c1 = f.cs[3 + 4 * d], s1 = f.sn[3 + 4 * d];
+            const double c2 = f.cs[4 + 4 * d], s2 = f.sn[4 + 4 * d];
+            const double c3 = f.cs[5 + 4 * d], s3 = f.sn[5 + 4 * d];
+            const double c4 = f.cs[6 + 4 * d], s4 = f.sn[6 + 4 * d];
+            const double L1 = H->L[d][1], L2 = H->L[d][2], L3 = H->L[d][3];
+            const double tc = H->twc[d], ts = H->tws[d];
+            // Columns 0, 1, 3 of A*B with A = [[c1,0,-s1,0],[s1,0,c1,0],[0,-1,0,0]] and
+            // B = [[c2,-s2*tc,s2*ts,L1*c2],[s2,c2*tc,-c2*ts,L1*s2],[0,ts,tc,0]]
+            // (thumbmodel.cpp:144-153; fingers tc = 1, ts = 0, fingermodel.cpp:137-145).
+            // Each entry is the reference's k-ordered sum with its exact-zero terms dropped.
+            const double b01 = -s2 * tc, b11 = c2 * tc, L1c2 = L1 * c2, L1s2 = L1 * s2;
+            const double AB00 = c1 * c2, AB10 = s1 * c2, AB20 = -s2;
+            const double AB01 = c1 * b01 + (-s1) * ts, AB11 = s1 * b01 + c1 * ts, AB21 = -b11;
+            const double AB03 = c1 * L1c2, AB13 = s1 * L1c2, AB23 = -L1s2;
+            const double cz = f.cs[0], sz = f.sn[0], cy = f.cs[1], sy = f.sn[1];
+            const double cxr = f.cs[2], sxr = f.sn[2];
+            double z0, z1, z2;  // row r of Rz
+            if (r == 0) { z0 = cz; z1 = -sz; z2 = 0; }
+            else if (r == 1) { z0 = sz; z1 = cz; z2 = 0; }
+            else { z0 = 0; z1 = 0; z2 = 1; }
+            // (Rz*Ry) row r, Ry = [[cy,0,sy],[0,1,0],[-sy,0,cy]]
+            const double q0 = z0 * cy + z2 * (-sy);
+            const double q1 = z1;
+            const double q2 = z0 * sy + z2 * cy;
+            // Tgb row r = q * Rx, Rx = [[1,0,0],[0,cx,-sx],[0,sx,cx]]; cur0 = T00*Tgb
+            const double g0 = q0;
+            const double g1 = q1 * cxr + q2 * sxr;
+            const double g2 = q1 * (-sxr) + q2 * cxr;
+            // cur1 = cur0 * F  (rotation about z + translation L0); its translation is X1 + u
+            const double h0 = g0 * H->Fc[d] + g1 * H->Fs[d];
+            const double h1 = g0 * (-H->Fs[d]) + g1 * H->Fc[d];
+            const double h2 = g2;
+            X1 = g0 * H->FLc[d] + g1 * H->FLs[d];
+            X0 = h0 * H->T10x[d] + h1 * H->T10y[d];  // (cur*T10) at i == 1
+            // cur2 = cur1 * AB
+            const double k0 = (h0 * AB00 + h1 * AB10) + h2 * AB20;
+            const double k1 = (h0 * AB01 + h1 * AB11) + h2 * AB21;
+            X2 = (h0 * AB03 + h1 * AB13) + h2 * AB23;
+            // cur3 = cur2 * C3, then the translation of cur3 * C4
+            const double m0 = k0 * c3 + k1 * s3;
+            const double m1 = k0 * (-s3) + k1 * c3;
+            X3 = k0 * (L2 * c3) + k1 * (L2 * s3);
+            X4 = m0 * (L3 * c4) + m1 * (L3 * s4);
+            if (MODE == FK_STORE_X) {
+                X->x[l][0] = X0;
+                X->x[l][1] = X1;
+                X->x[l][2] = X2;
+                X->x[l][3] = X3;
+                X->x[l][4] = X4;
+            }
+        }
+        const double J1 = X1 + u;
+        const double J0 = X0 + J1;
+        const double J2 = X2 + J1;
+        const double J3 = X3 + J2;
+        const double J4 = X4 + J3;
         f.J[d][0][r] = J0;
         f.J[d][1][r] = J1;
         f.J[d][2][r] = J2;
@@ -199,6 +231,10 @@ __device__ __forceinline__ void fk_wave(FkSm &f, const DevHand *__restrict__ H) 
     }
     wave_sync();
     sc.lap(14);
+}
+
+__device__ __forceinline__ void fk_wave(FkSm &f, const DevHand *__restrict__ H) {
+    fk_wave_t<FK_FULL>(f, H, nullptr);
 }
 
 // ---------------------------------------------------------------- reductions
@@ -523,11 +559,15 @@ __device__ __forceinline__ double eval_block(Smem &sm, const DevObs &o, const Cl
 // One wave evaluates cal_cost2(f.th, match, false): FK, frozen alignment over the
 // whole cloud, depth, collision; wave-local synchronisation only.  All lanes return
 // the total.
+// Xt != nullptr: f.th differs from the theta of Xt only in the global position
+// (FK_TRANSLATE).
 __device__ __forceinline__ double eval_wave_frozen(FkSm &f, const DevObs &o,
                                                    const CloudView &cv,
                                                    const DevHand *__restrict__ H,
-                                                   const int32_t *__restrict__ match) {
-    fk_wave(f, H);
+                                                   const int32_t *__restrict__ match,
+                                                   FkX *Xt = nullptr) {
+    if (Xt) fk_wave_t<FK_TRANSLATE>(f, H, Xt);
+    else fk_wave(f, H);
     StampClock sc;
     sc.start();
     const int l = threadIdx.x & 63;

@@ -633,6 +633,7 @@ struct __align__(16) RefineSm {
     double red[16][4];
     double x0[32], g[32], p[32];
     double f[RF_NW];
+    FkX X;  // rotation-only joint terms of x0 (refine block 2: translation steps)
 };
 
 // Goldstein bracket update (PSO.cpp:459-474), shared by the speculating waves and the walk.
@@ -655,7 +656,8 @@ __device__ __forceinline__ void gold_down(double a, double &b, double &alpha) {
 __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const CloudView &cv,
                                             const DevHand *__restrict__ H,
                                             const int32_t *__restrict__ match, double fk,
-                                            double gp, int &evals, double *f_acc) {
+                                            double gp, int &evals, double *f_acc,
+                                            FkX *Xt = nullptr) {
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
     StampClock sc;
     sc.start();
@@ -673,7 +675,7 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
             }
             if (l < HPE_DOF) rs.w[w].th[l] = rs.x0[l] + al2 * rs.p[l];
             wave_sync();
-            const double f = eval_wave_frozen(rs.w[w], o, cv, H, match);
+            const double f = eval_wave_frozen(rs.w[w], o, cv, H, match, Xt);
             if (l == 0) rs.f[w] = f;
         }
         __syncthreads();
@@ -782,6 +784,18 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
     const double e = 1e-5;  // cal_grad step (PSO.cpp:195)
     for (int blk = 0; blk < 2; ++blk) {
         const int lo = 3 * blk, hi = 3 * blk + 2;  // start_idx/end_idx (PSO.cpp:226-227)
+        // Block 2 moves only the global position u = x0[3..5]: every FK of the block is
+        // the stored rotation terms of x0 plus u (FK_TRANSLATE, bit-identical).
+        FkX *Xt = nullptr;
+        if (blk == 1) {
+            if (w == 0) {
+                if (l < HPE_DOF) rs.w[0].th[l] = rs.x0[l];
+                wave_sync();
+                fk_wave_t<FK_STORE_X>(rs.w[0], H, &rs.X);
+            }
+            __syncthreads();
+            Xt = &rs.X;
+        }
         double tol = 1;
         int cnt = 0, iter = 0;
         while (tol > 1e-6 && iter < 15 && cnt < 1) {
@@ -791,7 +805,10 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
             if (!base_valid) {
                 if (t < HPE_DOF) rs.base.th[t] = rs.x0[t];
                 __syncthreads();
-                if (w == 0) fk_wave(rs.base, H);
+                if (w == 0) {
+                    if (Xt) fk_wave_t<FK_TRANSLATE>(rs.base, H, Xt);
+                    else fk_wave(rs.base, H);
+                }
                 __syncthreads();
             }
             double dep = (t < HPE_NS) ? depth_term(rs.base, t, o, H) : 0.0;
@@ -807,7 +824,7 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
                 if (l < HPE_DOF)
                     rs.w[w].th[l] = (l == d) ? ((w & 1) ? rs.x0[l] - e : rs.x0[l] + e) : rs.x0[l];
                 wave_sync();
-                const double f = eval_wave_frozen(rs.w[w], o, cv, H, match);
+                const double f = eval_wave_frozen(rs.w[w], o, cv, H, match, Xt);
                 if (l == 0) rs.f[w] = f;
             }
             __syncthreads();
@@ -828,7 +845,7 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
             }
             const double gp = v1 + v2;
             // goldstein(x0, grad, matchId, f_k, optfunc, tk, 30)
-            const double tk = gold_tree(rs, o, cv, H, match, fk, gp, evals, nullptr);
+            const double tk = gold_tree(rs, o, cv, H, match, fk, gp, evals, nullptr, Xt);
             sc.lap(22);
             if (tk == 0) cnt += 1;
             {  // tol = sqrt(sum(grad % grad)): arrayops::accumulate over the squares

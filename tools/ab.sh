@@ -4,7 +4,7 @@
 set -o pipefail
 A=${1:-libhpe_base.so}
 R=${2:-2}
-mkdir -p gpurun_out/ab
+rm -rf gpurun_out/ab; mkdir -p gpurun_out/ab
 for r in $(seq 1 $R); do
   for v in "$A" libhpe.so; do
     tag=$(basename $v .so)_$r
