@@ -647,17 +647,207 @@ __device__ __forceinline__ void gold_down(double a, double &b, double &alpha) {
     alpha = 0.5 * (a + alpha);
 }
 
+// ---------------------------------------------------------------- multi-workgroup refine
+// For clouds larger than RF_STAGE_MAX one CU is throughput-bound (every Goldstein round is
+// seven frozen alignments of the whole cloud), so the refine launch adds Q helper
+// workgroups.  Workgroup 0 keeps the whole serial algorithm; each batch of evaluations
+// (the correspondence eval of x0, the gradient pairs, a Goldstein round) is published as
+// a job.  Helper h owns cloud slice h (and its matchId, written by the correspondence
+// job and read back by the same workgroup), computes the nodes' FK itself and returns one
+// partial alignment sum per node.  Workgroup 0 computes depth + collision meanwhile and
+// sums the partials in helper order (deterministic).  Hand-off per the G16 recipe:
+// stores drained, barrier, agent release, counter; one-lane agent acquire, barrier.
+// Every wait is bounded (~2 s): on a timeout the launch ends early with *err set.
+#define MW_SPIN_MAX (1 << 21)
+
+__device__ __forceinline__ bool mw_wait_geq(unsigned *p, unsigned v) {
+    for (int i = 0; i < MW_SPIN_MAX; ++i) {
+        if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= v) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            return true;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return false;
+}
+
+struct MwLeader {
+    DevMw mw;
+    unsigned k;   // jobs published so far
+    bool failed;  // a wait timed out: stop issuing work
+};
+
+// Workgroup 0: publish the next job (CORR: theta = rs.x0; FROZEN: rs.w[0..nn).th).
+__device__ void mw_publish(MwLeader &ml, RefineSm &rs, int type, int nn) {
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    if (type == MW_JOB_CORR) {
+        if (t < HPE_DOF) ml.mw.job->th[0][t] = rs.x0[t];
+    } else if (type == MW_JOB_FROZEN) {
+        if (w < nn && l < HPE_DOF) ml.mw.job->th[w][l] = rs.w[w].th[l];
+    }
+    if (t == 0) {
+        ml.mw.job->type = type;
+        ml.mw.job->nnodes = nn;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    ml.k += 1;
+    if (t == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_store(&ml.mw.ctr[0], ml.k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// Workgroup 0: wait until every helper has returned job ml.k.
+__device__ void mw_collect(MwLeader &ml, int *flag) {
+    if (threadIdx.x == 0) {
+        const bool ok = !ml.failed && mw_wait_geq(&ml.mw.ctr[1], ml.k * (unsigned)ml.mw.Q);
+        if (!ok) atomicExch(ml.mw.err, 1);
+        *flag = ok ? 1 : 0;
+    }
+    __syncthreads();
+    if (!*flag) ml.failed = true;
+}
+
+// Node w's alignment sum: the Q partials folded by one wave in a fixed order.
+__device__ __forceinline__ double mw_sum(const MwLeader &ml, int w) {
+    const int l = threadIdx.x & 63;
+    const double v = (l < ml.mw.Q) ? ml.mw.part[l * MW_MAX_NODES + w] : 0.0;
+    return wave_sum(v);
+}
+
+// rs.f[w] = cal_cost2(rs.w[w].th, matchId, false) for w < nn; each wave has written its
+// own rs.w[w].th.  Ends with a workgroup barrier.
+template <bool MW>
+__device__ __forceinline__ void eval_nodes(RefineSm &rs, int nn, const DevObs &o, const CloudView &cv,
+                                           const DevHand *__restrict__ H,
+                                           const int32_t *__restrict__ match, FkX *Xt,
+                                           MwLeader *ml, int *flag) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    if (!MW) {
+        if (w < nn) {
+            wave_sync();
+            const double f = eval_wave_frozen(rs.w[w], o, cv, H, match, Xt);
+            if (l == 0) rs.f[w] = f;
+        }
+        __syncthreads();
+        return;
+    }
+    mw_publish(*ml, rs, MW_JOB_FROZEN, nn);
+    double dep = 0.0, co = 0.0;
+    if (w < nn) {  // depth + collision here while the helpers align
+        if (Xt) fk_wave_t<FK_TRANSLATE>(rs.w[w], H, Xt);
+        else fk_wave(rs.w[w], H);
+        dep = (l < HPE_NS) ? depth_term(rs.w[w], l, o, H) : 0.0;
+        co = collide_term(rs.w[w], l, H) + collide_term(rs.w[w], l + 64, H) +
+             ((l < 16) ? collide_term(rs.w[w], l + 128, H) : 0.0);
+        wave_sum2(dep, co);
+    }
+    mw_collect(*ml, flag);
+    if (w < nn) {
+        const double al = mw_sum(*ml, w);
+        if (l == 0) rs.f[w] = ml->failed ? __builtin_nan("") : (al * o.lambda + dep) + co;
+    }
+    __syncthreads();
+}
+
+// f_k = cal_cost2(x0, matchId, true) with the spheres of x0 in rs.base.
+template <bool MW>
+__device__ __forceinline__ double eval_corr(RefineSm &rs, const DevObs &o, const CloudView &cv,
+                                            const DevHand *__restrict__ H, int32_t *__restrict__ match,
+                                            MwLeader *ml, int *flag) {
+    const int t = threadIdx.x;
+    if (MW) mw_publish(*ml, rs, MW_JOB_CORR, 1);
+    double dep = (t < HPE_NS) ? depth_term(rs.base, t, o, H) : 0.0;
+    double al = MW ? 0.0 : search_align<RF_NT, true>(rs.base, cv, H, match, load_pt(cv, t));
+    double co = (t < 144) ? collide_term(rs.base, t, H) : 0.0;
+    block_sum3<RF_NT>(rs.red, al, dep, co);  // also publishes matchId to the block
+    if (MW) {
+        mw_collect(*ml, flag);
+        al = mw_sum(*ml, 0);
+        if (ml->failed) return __builtin_nan("");
+    }
+    return (al * o.lambda + dep) + co;
+}
+
+// Helper workgroup h of a multi-workgroup refine launch: serve jobs until EXIT.
+__device__ void mw_helper(const DevMw &mw, int h, const DevObs *__restrict__ og,
+                          const DevHand *__restrict__ Hg, int32_t *__restrict__ match_g) {
+    __shared__ FkSm nodes[MW_MAX_NODES];
+    __shared__ DevHand hs;
+    __shared__ double red[16][4];
+    __shared__ int sh[2];
+    const DevObs o = *og;
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    for (int q = t; q < (int)(sizeof(DevHand) / 8); q += RF_NT)
+        ((double *)&hs)[q] = ((const double *)Hg)[q];
+    const DevHand *__restrict__ H = &hs;
+    const int Q = mw.Q, per = (o.n + Q - 1) / Q;
+    const int s0 = min(h * per, o.n), s1 = min(s0 + per, o.n);
+    const CloudView cs{o.cx + s0, o.cy + s0, o.cz + s0, s1 - s0};
+    int32_t *ms = match_g + s0;
+    __syncthreads();
+    for (unsigned k = 1;; ++k) {
+        if (t == 0) {
+            int type = -1, nn = 0;
+            if (mw_wait_geq(&mw.ctr[0], k)) {
+                type = mw.job->type;
+                nn = mw.job->nnodes;
+            } else {
+                atomicExch(mw.err, 1);
+            }
+            sh[0] = type;
+            sh[1] = nn;
+        }
+        __syncthreads();
+        const int type = sh[0], nn = sh[1];
+        if (type != MW_JOB_CORR && type != MW_JOB_FROZEN) {
+            // the last helper out resets the counters for the next launch
+            if (type == MW_JOB_EXIT && t == 0 && atomicAdd(&mw.ctr[2], 1u) == (unsigned)Q - 1) {
+                mw.ctr[0] = 0u;
+                mw.ctr[1] = 0u;
+                mw.ctr[2] = 0u;
+            }
+            return;
+        }
+        if (type == MW_JOB_CORR) {  // search + alignment over the slice, matchId stored
+            if (t < HPE_DOF) nodes[0].th[t] = mw.job->th[0][t];
+            __syncthreads();
+            if (w == 0) fk_wave(nodes[0], H);
+            __syncthreads();
+            double al = search_align<RF_NT, true>(nodes[0], cs, H, ms, load_pt(cs, t));
+            double z1 = 0.0, z2 = 0.0;
+            block_sum3<RF_NT>(red, al, z1, z2);
+            if (t == 0) mw.part[h * MW_MAX_NODES] = al;
+        } else if (w < nn) {  // one node per wave, frozen matchId of the slice
+            if (l < HPE_DOF) nodes[w].th[l] = mw.job->th[w][l];
+            wave_sync();
+            fk_wave(nodes[w], H);
+            const double al = wave_sum(align_frozen(nodes[w], cs, H, ms, l, 64));
+            if (l == 0) mw.part[h * MW_MAX_NODES + w] = al;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            atomicAdd(&mw.ctr[1], 1u);
+        }
+    }
+}
+
 // goldstein(x, g, matchId, f_k, optfunc, tk, 30) (PSO.cpp:438-480) along rs.p from rs.x0
 // with frozen correspondences, speculated RF_DEPTH levels per round: wave w evaluates tree
 // node w + 1 (root = current alpha, child 2n = "f1 > armijo" branch, 2n + 1 = "f1 <
 // goldstein" branch) and the walk replays the serial rules.  Returns tk (0 after 30
 // rejected trials); the accepted node's spheres are copied into rs.base and its cost to
 // *f_acc.  evals grows by the serial evaluation count.
+template <bool MW = false>
 __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const CloudView &cv,
                                             const DevHand *__restrict__ H,
                                             const int32_t *__restrict__ match, double fk,
                                             double gp, int &evals, double *f_acc,
-                                            FkX *Xt = nullptr) {
+                                            FkX *Xt = nullptr, MwLeader *ml = nullptr,
+                                            int *flag = nullptr) {
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
     StampClock sc;
     sc.start();
@@ -674,11 +864,9 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
                 else gold_down(a, b, al2);
             }
             if (l < HPE_DOF) rs.w[w].th[l] = rs.x0[l] + al2 * rs.p[l];
-            wave_sync();
-            const double f = eval_wave_frozen(rs.w[w], o, cv, H, match, Xt);
-            if (l == 0) rs.f[w] = f;
         }
-        __syncthreads();
+        eval_nodes<MW>(rs, (1 << RF_DEPTH) - 1, o, cv, H, match, Xt, ml, flag);
+        if (MW && ml->failed) break;  // the launch is ending early (DevMw::err)
         int node = 1;
         accepted = -1;
         for (int lev = 0; lev < RF_DEPTH && !done; ++lev) {
@@ -738,18 +926,25 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
 // others, when present, prepare the NEXT frame meanwhile (hpe_prep.hpp) on
 // CUs this single-workgroup refine leaves idle -- one launch, one stream, no cross-queue
 // dependencies in the frame loop.
-template <bool STAGED>
+// MW (clouds > RF_STAGE_MAX): workgroups 1..mw.Q are the helpers of the multi-workgroup
+// form above; the preparation workgroups follow them.
+template <bool STAGED, bool MW = false>
 __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, const DevObs *__restrict__ og,
                                                   const DevHand *__restrict__ Hg,
                                                   int32_t *__restrict__ match_g,
                                                   int *__restrict__ evals_out, int do_refine,
-                                                  PrepArgs pa) {
+                                                  PrepArgs pa, DevMw mw) {
     extern __shared__ __align__(16) unsigned char dyn[];  // staged cloud + matchId / prep
+    const int nhelp = MW ? mw.Q : 0;
+    if (MW && blockIdx.x >= 1 && (int)blockIdx.x <= nhelp) {
+        if (do_refine) mw_helper(mw, blockIdx.x - 1, og, Hg, match_g);
+        return;
+    }
     if (blockIdx.x >= 1) {
         const unsigned long long t0 = HPE_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
-        prep_workgroup(pa, blockIdx.x - 1, dyn);
+        prep_workgroup(pa, blockIdx.x - 1 - nhelp, dyn);
         if (HPE_STAMPS && threadIdx.x == 0) {  // diagnostic build: prep workgroup spans
-            const int k = (blockIdx.x - 1 < PREP_BANDS) ? 24 : 25;
+            const int k = ((int)blockIdx.x - 1 - nhelp < PREP_BANDS) ? 24 : 25;
             atomicAdd(&hpe_stamps[k], __builtin_amdgcn_s_memtime() - t0);
             atomicAdd(&hpe_stamps[32 + k], 1ull);
         }
@@ -776,6 +971,8 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
         match = (int32_t *)(cz + o.n);
     }
     if (t < HPE_DOF) rs.x0[t] = x0g[t];
+    __shared__ int mwflag;
+    MwLeader ml{mw, 0u, false};
     __syncthreads();
     StampClock sc;
     sc.start();
@@ -798,7 +995,7 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
         }
         double tol = 1;
         int cnt = 0, iter = 0;
-        while (tol > 1e-6 && iter < 15 && cnt < 1) {
+        while (tol > 1e-6 && iter < 15 && cnt < 1 && !(MW && ml.failed)) {
             // f_k = cal_cost2(x0, matchId, true).  The spheres of x0 are already in rs.base
             // when x0 is the accepted Goldstein point of the previous iteration
             // (x0 + tk*p == x0 - tk*g bitwise) or an unchanged x0.
@@ -811,11 +1008,7 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
                 }
                 __syncthreads();
             }
-            double dep = (t < HPE_NS) ? depth_term(rs.base, t, o, H) : 0.0;
-            double al = search_align<RF_NT, true>(rs.base, cv, H, match, load_pt(cv, t));
-            double co = (t < 144) ? collide_term(rs.base, t, H) : 0.0;
-            block_sum3<RF_NT>(rs.red, al, dep, co);  // also publishes matchId to the block
-            const double fk = (al * o.lambda + dep) + co;
+            const double fk = eval_corr<MW>(rs, o, cv, H, match, &ml, &mwflag);
             ++evals;
             sc.lap(20);
             // cal_grad: x0 +/- e along the 3 block dims, one wave per evaluation
@@ -823,11 +1016,8 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
                 const int d = lo + (w >> 1);
                 if (l < HPE_DOF)
                     rs.w[w].th[l] = (l == d) ? ((w & 1) ? rs.x0[l] - e : rs.x0[l] + e) : rs.x0[l];
-                wave_sync();
-                const double f = eval_wave_frozen(rs.w[w], o, cv, H, match, Xt);
-                if (l == 0) rs.f[w] = f;
             }
-            __syncthreads();
+            eval_nodes<MW>(rs, 6, o, cv, H, match, Xt, &ml, &mwflag);
             evals += 6;
             if (t < HPE_DOF) {
                 const double g = (t >= lo && t <= hi)
@@ -845,7 +1035,7 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
             }
             const double gp = v1 + v2;
             // goldstein(x0, grad, matchId, f_k, optfunc, tk, 30)
-            const double tk = gold_tree(rs, o, cv, H, match, fk, gp, evals, nullptr, Xt);
+            const double tk = gold_tree<MW>(rs, o, cv, H, match, fk, gp, evals, nullptr, Xt, &ml, &mwflag);
             sc.lap(22);
             if (tk == 0) cnt += 1;
             {  // tol = sqrt(sum(grad % grad)): arrayops::accumulate over the squares
@@ -864,6 +1054,7 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
             sc.lap(23);
         }
     }
+    if (MW) mw_publish(ml, rs, MW_JOB_EXIT, 0);
     if (t < HPE_DOF) x0g[t] = rs.x0[t];
     if (t == 0 && evals_out) *evals_out = evals;
 }

@@ -90,3 +90,21 @@ struct DevOpt {
     int P, G, n_cap;
     double w, c1, c2;
 };
+
+// Multi-workgroup refine (clouds too large for one CU): workgroup 0 runs refine_init_pose
+// and publishes each batch of evaluations as a job; Q helper workgroups each own a fixed
+// slice of the cloud (and of matchId) and return per-node partial alignment sums.
+#define MW_MAX_Q 64
+#define MW_MAX_NODES 8
+enum { MW_JOB_CORR = 1, MW_JOB_FROZEN = 2, MW_JOB_EXIT = 3 };
+struct MwJob {
+    int type, nnodes, pad[2];
+    double th[MW_MAX_NODES][32];
+};
+struct DevMw {
+    MwJob *job;
+    double *part;    // [MW_MAX_Q][MW_MAX_NODES] partial alignment sums
+    unsigned *ctr;   // [0] job sequence, [1] helper completions, [2] helper exits
+    int *err;        // set when a wait times out (the launch then ends early)
+    int Q;
+};

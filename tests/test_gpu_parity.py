@@ -229,6 +229,32 @@ def test_refine_init_pose(oracle, ora_hand, gpu_hand, np_hand):
     np.testing.assert_allclose(x, x_ref, rtol=0, atol=1e-6)
 
 
+@pytest.mark.parametrize("mw", ["1", "0"])
+def test_refine_full_cloud(oracle, ora_hand, np_hand, mw, monkeypatch):
+    """refine_init_pose on a full-resolution cloud (> 2048 points): the multi-workgroup
+    form (mw=1: 64 helper workgroups own cloud slices, partial sums folded in a fixed
+    order) and the single-workgroup form (HPE_REFINE_MW=0) both match the oracle, with
+    the reference's evaluation count."""
+    import hpe
+    monkeypatch.setenv("HPE_REFINE_MW", mw)
+    gh = hpe.reference_hand(device=0)  # the context reads HPE_REFINE_MW at creation
+    truth = hand_data.trajectory(2, seed=4)[1]
+    d = oracle_np.render_depth_mm(np_hand, truth)
+    obs, om = _obs_pair(oracle, gh, d, downsample=False)
+    assert obs.n > 2048
+    cf = hpe.costfunc(gh, om)
+    x0 = oracle_np.X0.copy()
+    x_ref, ev_ref = oracle.refine(ora_hand, obs, x0)
+    pso = hpe.PSO()
+    x = x0.copy()
+    pso.refine_init_pose(x, cf)
+    assert pso.last_refine_evals == ev_ref
+    np.testing.assert_allclose(x, x_ref, rtol=0, atol=1e-6)
+    x2 = x0.copy()  # deterministic: a second call gives the same bits
+    pso.refine_init_pose(x2, cf)
+    assert np.array_equal(x, x2)
+
+
 def test_track_sequence(oracle, ora_hand, gpu_hand, np_hand):
     """test_full's loop (testmodel.cpp:117-139) on 3 synthetic frames, 32 particles."""
     import hpe
