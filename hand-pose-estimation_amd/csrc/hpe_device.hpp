@@ -64,7 +64,7 @@ struct StampClock {
 
 // Per-evaluating-wave LDS workspace.
 struct __align__(16) FkSm {
-    float4 Sf[HPE_NS];       // fp32 centres for the search
+    float Sp[3][HPE_NS];     // fp32 centres for the search, one row per coordinate
     double S[HPE_NS][3];     // fp64 centres, y/z negated (handmodel.cpp:288)
     double J[5][5][3];       // joints per digit (hand_joints source)
     double th[32];           // the particle
@@ -226,7 +226,7 @@ __device__ __forceinline__ void fk_wave_t(FkSm &f, const DevHand *__restrict__ H
             const double v = H->wa[s] * f.J[d][a][r] + H->wb[s] * f.J[d][a + 1][r];
             const double vs = (r == 0) ? v : v * -1;
             f.S[s][r] = vs;
-            ((float *)&f.Sf[s])[r] = (float)vs;
+            f.Sp[r][s] = (float)vs;
         }
     }
     wave_sync();
@@ -421,7 +421,8 @@ __device__ __forceinline__ double search_align(const FkSm &f, const CloudView &c
     if (gt < 0) gt = threadIdx.x;
     double acc = 0.0;
     const int h = gt & 1;
-    const float4 *Sf = f.Sf + 24 * h;
+    typedef float f2 __attribute__((ext_vector_type(2)));  // packed fp32 (v_pk_*_f32)
+    const float *SX = f.Sp[0] + 24 * h, *SY = f.Sp[1] + 24 * h, *SZ = f.Sp[2] + 24 * h;
     for (int it = gt; it < 2 * cv.n; it += NT) {
         const int p = it >> 1;
         const Pt q = (it == gt) ? pre : load_pt(cv, it);
@@ -429,12 +430,16 @@ __device__ __forceinline__ double search_align(const FkSm &f, const CloudView &c
         const float qx = (float)X, qy = (float)Y, qz = (float)Z;
         float d2[24];
         float m = __builtin_inff();
+        const f2 q2x = {qx, qx}, q2y = {qy, qy}, q2z = {qz, qz};
 #pragma unroll
-        for (int j = 0; j < 24; ++j) {
-            const float4 s = Sf[j];
-            const float t0 = qx - s.x, t1 = qy - s.y, t2 = qz - s.z;
-            d2[j] = (t0 * t0 + t1 * t1) + t2 * t2;
-            m = fminf(m, d2[j]);
+        for (int j = 0; j < 24; j += 2) {  // two spheres per packed op, same IEEE results
+            const f2 sx = *(const f2 *)(SX + j), sy = *(const f2 *)(SY + j),
+                     sz = *(const f2 *)(SZ + j);
+            const f2 t0 = q2x - sx, t1 = q2y - sy, t2 = q2z - sz;
+            const f2 d = (t0 * t0 + t1 * t1) + t2 * t2;
+            d2[j] = d.x;
+            d2[j + 1] = d.y;
+            m = fminf(m, fminf(d.x, d.y));
         }
         m = fminf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0xB1, 0xf, 0xf,
                                                                false)));  // partner lane t^1
@@ -521,7 +526,7 @@ __device__ __forceinline__ CloudView obs_cloud(const DevObs &o) {
 // Whole-block evaluation of the particle in sm.fk.th (wave 0 does FK, NT threads the
 // search).  Every thread returns the total; terms (align, depth, collision) go to
 // sm.dscal[0..2].
-// FK = false: the caller has already placed the centres in sm.fk.S / Sf (hpe_eval_spheres).
+// FK = false: the caller has already placed the centres in sm.fk.S / Sp (hpe_eval_spheres).
 template <int MODE, int NT, bool FK = true>
 __device__ __forceinline__ double eval_block(Smem &sm, const DevObs &o, const CloudView &cv,
                                              const DevHand *__restrict__ H,

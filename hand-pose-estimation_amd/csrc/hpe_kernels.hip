@@ -86,7 +86,7 @@ __global__ __launch_bounds__(HPE_NT) void k_eval_spheres(const double *__restric
         const int s = t / 3, r = t - 3 * s;
         const double v = S[(size_t)i * 3 * HPE_NS + t];
         sm.fk.S[s][r] = v;
-        ((float *)&sm.fk.Sf[s])[r] = (float)v;
+        sm.fk.Sp[r][s] = (float)v;
     }
     const CloudView cv = obs_cloud(o);
     const Pt pre = load_pt(cv, t);

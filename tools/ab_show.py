@@ -4,7 +4,7 @@ import glob
 import json
 import sys
 
-for f in sorted(glob.glob("gpurun_out/ab/bench_*.log")):
+for f in sorted(glob.glob("gpurun_out/ab/bench*.log")):
     for line in open(f):
         if line.startswith("{"):
             d = json.loads(line)
