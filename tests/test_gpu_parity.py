@@ -297,6 +297,37 @@ def test_edge_small_clouds(oracle, ora_hand, gpu_hand):
                                oracle.eval_costs(ora_hand, obs, oracle_np.X0[None]), rtol=RTOL)
 
 
+def test_edge_empty_frame_optimisers(oracle, ora_hand, gpu_hand):
+    """An all-background frame (N = 0): lambda = 48/0, so every cost is NaN as in the
+    reference (costfunc.cpp:372); no pbest ever improves, gbest stays zeros (PSO.cpp:546),
+    refine's searches fail and leave x0 unchanged with the reference's eval count."""
+    import hpe
+    d = np.zeros((240, 320), np.float32)
+    obs = oracle.preprocess(d, downsample=False)
+    assert obs.n == 0
+    om = hpe.observedmodel(); om.set_depth_mm(d)
+    cf = hpe.costfunc(gpu_hand, om)
+    ub, lb, sd = oracle_np.reference_bounds()
+    pso = hpe.PSO()
+    pso.set_pso_params(ub, lb, sd, 0.7298, 1.49618, 1.49618, 3, 1e-8, 1e-8)
+    x0 = oracle_np.X0.copy()
+    bp = np.zeros(26)
+    pso.pso_evolve(cf, x0, 8, bp)
+    rb, rc, _ = oracle.pso_evolve(ora_hand, obs, x0, 8, 3, lb, ub, sd, seed=1000)
+    np.testing.assert_array_equal(bp, rb)
+    assert pso.last_gbest_cost == rc
+    x = x0.copy()
+    pso.refine_init_pose(x, cf)
+    xr, evr = oracle.refine(ora_hand, obs, x0)
+    np.testing.assert_array_equal(x, xr)
+    assert pso.last_refine_evals == evr
+    pso.pso_optimise(cf, x0, 4, bp)
+    ob, oc, _ = oracle.pso_optimise(ora_hand, obs, x0, 4, 3, lb, ub, sd, 0.7298, 1.49618,
+                                    1.49618, seed=1000)
+    np.testing.assert_array_equal(bp, ob)
+    assert pso.last_gbest_cost == oc
+
+
 @pytest.mark.parametrize("P,maxiter", [(32, 11), (7, 4), (1, 3), (1030, 3)])
 def test_pso_evolve_wave_form(oracle, ora_hand, np_hand, P, maxiter, monkeypatch):
     """The one-wave-per-particle generation kernels (used for large swarms) against the
