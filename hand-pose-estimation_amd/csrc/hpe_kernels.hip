@@ -538,12 +538,20 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
 // Last end-of-generation update and bestp = gbest_pos (PSO.cpp:864-882).  Replays the
 // gbest / count sequence from gmin[], finds the last improving generation g* and takes
 // particles.col(first argmin pcost) of that generation; resets gmin[] for the next call.
-__global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__restrict__ out) {
+// TAIL (a tracked frame, testmodel.cpp:130-132): the same block then evaluates
+// cal_cost(bestp) into out[26] -- eval_block as in k_eval, so the same bits -- and copies
+// the frame descriptor it used to obs_out (the API's "selected frame").
+template <bool TAIL = false>
+__global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__restrict__ out,
+                                                      const DevObs *__restrict__ og = nullptr,
+                                                      const DevHand *__restrict__ Hg = nullptr,
+                                                      DevObs *__restrict__ obs_out = nullptr) {
     constexpr int CH = 2048;  // generations staged per pass
     __shared__ Smem sm;
     __shared__ double gm[CH];
     __shared__ int tp[CH];
     const int t = threadIdx.x, G = sw.G, P = sw.P;
+    if (TAIL) stage_hand<HPE_NT>(sm.hand, Hg);
     double gcost = 1e100;
     int last = -1, count = 100;
     for (int base = 0; base <= G; base += CH) {
@@ -607,6 +615,17 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
     __syncthreads();
     if (t < HPE_DOF) sw.gpos[t] = out[t];
     for (int g = t; g <= G; g += HPE_NT) sw.gmin[g] = ~0ull;
+    if (TAIL) {
+        const DevObs o = *og;
+        if (t < HPE_DOF) sm.fk.th[t] = out[t];
+        if (obs_out && t < (int)(sizeof(DevObs) / 8))
+            ((unsigned long long *)obs_out)[t] = ((const unsigned long long *)og)[t];
+        const CloudView cv = obs_cloud(o);
+        const Pt pre = load_pt(cv, t);
+        __syncthreads();
+        const double c = eval_block<EV_COST, HPE_NT>(sm, o, cv, &sm.hand, nullptr, pre);
+        if (t == 0) out[HPE_DOF] = c;
+    }
 }
 
 // ------------------------------------------------------------------ refine

@@ -41,6 +41,8 @@ struct DevObs {
     double K[9];
 };
 
+static_assert(sizeof(DevObs) % 8 == 0, "DevObs is copied as 8-byte words");
+
 struct Sig {  // swarm scalars carried across generation kernels
     double gcost;
     int count;
