@@ -67,6 +67,14 @@ __device__ __forceinline__ int wave_prefix_min(int v) {
     v = min(v, __builtin_amdgcn_update_dpp(id, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
     return v;
 }
+// inclusive prefix minimum of five values in two levels of v_min3
+__device__ __forceinline__ void scan5_min(const int q[5], int p[5]) {
+    p[0] = q[0];
+    p[1] = min(q[0], q[1]);
+    p[2] = min(min(q[0], q[1]), q[2]);
+    p[3] = min(min(p[1], q[2]), q[3]);
+    p[4] = min(min(p[2], q[3]), q[4]);
+}
 // value of lane l-1 (lane 0: fill) / lane l+1 (lane 63: fill)
 __device__ __forceinline__ int from_left(int v, int fill) {
     return __builtin_amdgcn_update_dpp(fill, v, 0x138, 0xf, 0xf, false);  // wave_shr:1
@@ -272,24 +280,25 @@ __device__ __forceinline__ void prep_dt(const PrepArgs &a, unsigned char *lds) {
             const unsigned long long mw =
                 ((unsigned long long)msk[(pix0 >> 5) + 1] << 32) | msk[pix0 >> 5];
             const unsigned hb = (unsigned)(mw >> (pix0 & 31));
-            int pm = 0x7FFFFFFF, p[5];
+            int q[5], p[5];
 #pragma unroll
             for (int k = 0; k < 5; ++k) {
                 const int i = k + 2;
                 // grouped by weight: min over the LONG, DIAG and HV neighbours, then the add
                 const int mL = min(min(u2[i - 1], u2[i + 1]), min(u1[i - 2], u1[i + 2]));
                 const int mD = min(u1[i - 1], u1[i + 1]);
-                int av = min(min(mL + DT_LONG, mD + DT_DIAG), u1[i] + DT_HV);
-                av = ((hb >> k) & 1u) ? 0 : av;
-                pm = min(pm, av - DT_HV * (c0 + k));
-                p[k] = pm;
+                const int av = min(min(mL + DT_LONG, mD + DT_DIAG), u1[i] + DT_HV);
+                // hand pixel -> 0: bit k sign-extended, then av & ~mask in one v_bfi
+                const int m = __builtin_amdgcn_sbfe((int)hb, k, 1);
+                q[k] = (av & ~m) - DT_HV * (c0 + k);
             }
-            const int ex = from_left(wave_prefix_min(pm), 0x7FFFFFFF);  // lanes < l
+            scan5_min(q, p);  // p[k] = min(q[0..k]), depth 2
+            const int ex = from_left(wave_prefix_min(p[4]), 0x7FFFFFFF);  // lanes < l
             int T[5];
 #pragma unroll
             for (int k = 0; k < 5; ++k) {
-                const int c = c0 + k;
-                T[k] = min(min(p[k], ex) + DT_HV * c, DT_INIT + DT_HV * (c + 1));
+                // min(min(p, ex) + HV c, INIT + HV (c+1)) == min(p, ex, INIT + HV) + HV c
+                T[k] = min(min(p[k], ex), DT_INIT + DT_HV) + DT_HV * (c0 + k);
                 a.dtf[pix0 + k] = T[k];
             }
 #pragma unroll
@@ -318,22 +327,22 @@ __device__ __forceinline__ void prep_dt(const PrepArgs &a, unsigned char *lds) {
         for (int r = H - 1; r >= 0; --r) {
 #pragma unroll
             for (int k = 0; k < 5; ++k) fn[k] = (r > 0) ? a.dtf[(r - 1) * W + cb - k] : 0;
-            int pm = 0x7FFFFFFF, p[5];
+            int q[5], p[5];
 #pragma unroll
             for (int k = 0; k < 5; ++k) {
                 const int i = k + 2;
                 const int mL = min(min(d2[i - 1], d2[i + 1]), min(d1[i - 2], d1[i + 2]));
                 const int mD = min(d1[i - 1], d1[i + 1]);
                 const int bv = min(min(fw[k], mL + DT_LONG), min(mD + DT_DIAG, d1[i] + DT_HV));
-                pm = min(pm, bv - DT_HV * (5 * l + k));
-                p[k] = pm;
+                q[k] = bv - DT_HV * (5 * l + k);
             }
-            const int ex = from_left(wave_prefix_min(pm), 0x7FFFFFFF);
+            scan5_min(q, p);
+            const int ex = from_left(wave_prefix_min(p[4]), 0x7FFFFFFF);
             int T[5];
 #pragma unroll
             for (int k = 0; k < 5; ++k) {
                 const int j = 5 * l + k;
-                T[k] = min(min(p[k], ex) + DT_HV * j, DT_INIT + DT_HV * (j + 1));
+                T[k] = min(min(p[k], ex), DT_INIT + DT_HV) + DT_HV * j;
                 const float v = (float)T[k] * sc;
                 a.dt[r * W + cb - k] = v;
                 mx = v > mx ? v : mx;
