@@ -143,6 +143,29 @@ __device__ __forceinline__ double bits_to_f64(unsigned long long b) { return __l
 __device__ __forceinline__ unsigned long long f64_to_bits(double v) {
     return (unsigned long long)__double_as_longlong(v);
 }
+// The generation's minimum pbest cost (the gmin the next generation's topology decision
+// and k_pso_final read), sharded: particle i lowers cell i % GMIN_SHARDS.  All 256 blocks
+// of a launch hitting ONE address serialise their atomics at the memory side for ~2 us of
+// every generation; 32 cells on separate 128-B lines take 8 each.  Costs are >= 0 (or
+// NaN), so u64 order is value order, and the min over the shards is order-free.
+__device__ __forceinline__ unsigned long long *gmin_cell(const DevSwarm &sw, int g, int s) {
+    return sw.gmin + ((size_t)g * GMIN_SHARDS + s) * GMIN_STRIDE;
+}
+__device__ __forceinline__ void gmin_lower(const DevSwarm &sw, int g, int i, double c) {
+    atomicMin(gmin_cell(sw, g, i % GMIN_SHARDS), f64_to_bits(c));
+}
+// min over generation g's shards by one whole wave, in every lane; NaN if none was written
+__device__ __forceinline__ double gmin_read(const DevSwarm &sw, int g) {
+    const int l = threadIdx.x & 63;
+    double m = (l < GMIN_SHARDS) ? bits_to_f64(*gmin_cell(sw, g, l)) : __builtin_nan("");
+    m = fmin(m, dpp_f64<0xB1>(m));
+    m = fmin(m, dpp_f64<0x4E>(m));
+    m = fmin(m, dpp_f64<0x141>(m));
+    m = fmin(m, dpp_f64<0x140>(m));
+    return fmin(fmin(readlane_f64(m, 0), readlane_f64(m, 16)),
+                fmin(readlane_f64(m, 32), readlane_f64(m, 48)));
+}
+
 __device__ __forceinline__ size_t ib_index(const DevSwarm &sw, int par, int var, int r, int slot) {
     return ((((size_t)par * 2 + var) * sw.P + r) * sw.K + slot) * IB_FIELDS;
 }
@@ -199,7 +222,7 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_init(DevSwarm sw, const double *
     const double c = eval_block<EV_COST, HPE_NT>(sm, o, cv, H, nullptr, pre);
     if (t == 0) {  // PSO.cpp:748-763; pbest costs are >= 0, so their bits order like values
         sw.pch[i] = c;
-        atomicMin(&sw.gmin[0], f64_to_bits(c));
+        gmin_lower(sw, 0, i, c);
     }
     push_inbox(sw, 0, i, q, lr, ls, 1, c, sm.fk.th);
 }
@@ -257,7 +280,7 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
             pbi = sw.pb[e];
         }
         const double pci = sw.pch[(size_t)(g - 1) * P + i];  // own pbest cost (uniform)
-        const double fmin = bits_to_f64(sw.gmin[g - 1]);     // all-ones (no value) is a NaN
+        const double fmin = gmin_read(sw, g - 1);  // NaN when no value was written
         const Sig pv = sw.sig[g > 1 ? g - 1 : 0];
         double tg[2] = {0, 0}, tc[2] = {0, 0};
         if (t < K) {
@@ -350,7 +373,7 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
     }
     if (t == 0) {
         sw.pch[(size_t)g * P + i] = pn;
-        atomicMin(&sw.gmin[g], f64_to_bits(pn));
+        gmin_lower(sw, g, i, pn);
     }
     __syncthreads();
     push_inbox(sw, g, i, q, lr, ls, q < 3 * IB_FIELDS ? g + 1 : topo, pn, sm.fk.th);
@@ -410,7 +433,7 @@ __global__ __launch_bounds__(PW_NT) void k_pso_init_w(DevSwarm sw, const double 
     if (!valid) return;
     if (l == 0) {
         sw.pch[i] = c;
-        atomicMin(&sw.gmin[0], f64_to_bits(c));
+        gmin_lower(sw, 0, i, c);
     }
 #pragma unroll
     for (int k = 0; k < 3; ++k) push_inbox(sw, 0, i, l + 64 * k, lr[k], ls[k], 1, c, f.th);
@@ -444,7 +467,7 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
         rg = philox_u01(sw.seed, ST_RG, g, ic, l);
     }
     const double pci = sw.pch[(size_t)(g - 1) * P + ic];
-    const double fmin = bits_to_f64(sw.gmin[g - 1]);
+    const double fmin = gmin_read(sw, g - 1);
     const Sig pv = sw.sig[g > 1 ? g - 1 : 0];
     double tg[2] = {0, 0}, tc[2] = {0, 0};
     if (l < K) {
@@ -525,7 +548,7 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
     }
     if (l == 0) {
         sw.pch[(size_t)g * P + i] = pn;
-        atomicMin(&sw.gmin[g], f64_to_bits(pn));
+        gmin_lower(sw, g, i, pn);
     }
     wave_sync();
 #pragma unroll
@@ -557,7 +580,10 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
     for (int base = 0; base <= G; base += CH) {
         // all loads of the pass at once, then a serial replay from LDS by thread 0
         for (int k = t; k < CH && base + k <= G; k += HPE_NT) {
-            gm[k] = bits_to_f64(sw.gmin[base + k]);  // all-ones (never written) is a NaN
+            double m = __builtin_nan("");  // all-ones (never written) is a NaN too
+            for (int c = 0; c < GMIN_SHARDS; ++c)
+                m = fmin(m, bits_to_f64(*gmin_cell(sw, base + k, c)));
+            gm[k] = m;
             tp[k] = (base + k >= 1) ? sw.sig[base + k].topo : -1;
         }
         __syncthreads();
@@ -614,7 +640,7 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
     if (t == 0) out[HPE_DOF] = gcost;
     __syncthreads();
     if (t < HPE_DOF) sw.gpos[t] = out[t];
-    for (int g = t; g <= G; g += HPE_NT) sw.gmin[g] = ~0ull;
+    for (int c = t; c < (G + 1) * GMIN_SHARDS; c += HPE_NT) sw.gmin[(size_t)c * GMIN_STRIDE] = ~0ull;
     if (TAIL) {
         const DevObs o = *og;
         if (t < HPE_DOF) sm.fk.th[t] = out[t];

@@ -56,13 +56,16 @@ struct Sig {  // swarm scalars carried across generation kernels
 // topologies of generation g+1 (rebuilt at g+1, or kept), so generation g+1 reads all
 // it needs from its own inbox in one round trip.
 #define IB_FIELDS 28  // tag, pbest cost, pbest position[26]
+#define GMIN_SHARDS 32  // atomicMin cells per generation
+#define GMIN_STRIDE 16  // u64 per cell: one 128-B line each
 struct DevSwarm {
     double *xh;               // (G+1) x P x 26   particle positions per generation
     double *pch;              // (G+1) x P        pbest costs per generation
     double *pb;               // P x 26           pbest positions (own particle only)
     double *v;                // P x 26           velocities (own particle only)
     double *inbox;            // 2 x 2 x P x K x IB_FIELDS  [g&1][kept, rebuilt][receiver][slot]
-    unsigned long long *gmin; // G+1              min pbest cost bits per generation (atomicMin)
+    unsigned long long *gmin; // (G+1) x GMIN_SHARDS cells (128-B apart): min pbest cost bits
+                              // per generation, particle i lowering shard i % GMIN_SHARDS
     Sig *sig;                 // G+1              gbest cost / count / topology per generation
     const double *normals;    // P x 26
     const int *outl;          // (G+1) x P x 3 x 2  (receiver, slot) of each link per topology
