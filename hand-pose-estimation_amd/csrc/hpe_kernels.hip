@@ -704,6 +704,7 @@ __device__ __forceinline__ void gold_down(double a, double &b, double &alpha) {
 // stores drained, barrier, agent release, counter; one-lane agent acquire, barrier.
 // Every wait is bounded (~2 s): on a timeout the launch ends early with *err set.
 #define MW_SPIN_MAX (1 << 21)
+static_assert(MW_MAX_Q % MW_DONE_SHARDS == 0, "helpers split evenly over the shards");
 
 __device__ __forceinline__ bool mw_wait_geq(unsigned *p, unsigned v) {
     for (int i = 0; i < MW_SPIN_MAX; ++i) {
@@ -743,10 +744,13 @@ __device__ void mw_publish(MwLeader &ml, RefineSm &rs, int type, int nn) {
     }
 }
 
-// Workgroup 0: wait until every helper has returned job ml.k.
+// Workgroup 0: wait until every helper has returned job ml.k (each completion shard has
+// counted Q / MW_DONE_SHARDS helpers per job).
 __device__ void mw_collect(MwLeader &ml, int *flag) {
     if (threadIdx.x == 0) {
-        const bool ok = !ml.failed && mw_wait_geq(&ml.mw.ctr[1], ml.k * (unsigned)ml.mw.Q);
+        bool ok = !ml.failed;
+        const unsigned want = ml.k * (unsigned)(ml.mw.Q / MW_DONE_SHARDS);
+        for (int s = 0; s < MW_DONE_SHARDS && ok; ++s) ok = mw_wait_geq(&ml.mw.ctr[32 * (1 + s)], want);
         if (!ok) atomicExch(ml.mw.err, 1);
         *flag = ok ? 1 : 0;
     }
@@ -848,10 +852,9 @@ __device__ void mw_helper(const DevMw &mw, int h, const DevObs *__restrict__ og,
         const int type = sh[0], nn = sh[1];
         if (type != MW_JOB_CORR && type != MW_JOB_FROZEN) {
             // the last helper out resets the counters for the next launch
-            if (type == MW_JOB_EXIT && t == 0 && atomicAdd(&mw.ctr[2], 1u) == (unsigned)Q - 1) {
-                mw.ctr[0] = 0u;
-                mw.ctr[1] = 0u;
-                mw.ctr[2] = 0u;
+            if (type == MW_JOB_EXIT && t == 0 &&
+                atomicAdd(&mw.ctr[32 * (1 + MW_DONE_SHARDS)], 1u) == (unsigned)Q - 1) {
+                for (int c = 0; c < MW_CTR_WORDS; c += 32) mw.ctr[c] = 0u;
             }
             return;
         }
@@ -875,7 +878,7 @@ __device__ void mw_helper(const DevMw &mw, int h, const DevObs *__restrict__ og,
         __syncthreads();
         if (t == 0) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            atomicAdd(&mw.ctr[1], 1u);
+            atomicAdd(&mw.ctr[32 * (1 + h % MW_DONE_SHARDS)], 1u);
         }
     }
 }

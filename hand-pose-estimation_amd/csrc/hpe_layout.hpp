@@ -88,7 +88,7 @@ struct DevOpt {
     double *gbest;            // 28: position, cost, count
     double *trace;            // [G] gbest cost after each generation
     int32_t *match;           // P x n_cap correspondences (clouds too large for LDS)
-    unsigned *ctr;            // arrival counter (reset by the last workgroup)
+    unsigned *ctr;            // sharded arrival counters (arrive_last_sharded)
     const double *normals;    // P x 26 (stream ST_OPT_NORMAL)
     const double *bounds;     // lb[26], ub[26], std[26]
     uint64_t seed;
@@ -101,6 +101,8 @@ struct DevOpt {
 // slice of the cloud (and of matchId) and return per-node partial alignment sums.
 #define MW_MAX_Q 64
 #define MW_MAX_NODES 8
+#define MW_DONE_SHARDS 8  // completion counters (MW_MAX_Q a multiple of it)
+#define MW_CTR_WORDS (32 * (MW_DONE_SHARDS + 2))
 enum { MW_JOB_CORR = 1, MW_JOB_FROZEN = 2, MW_JOB_EXIT = 3 };
 struct MwJob {
     int type, nnodes, pad[2];
@@ -109,7 +111,8 @@ struct MwJob {
 struct DevMw {
     MwJob *job;
     double *part;    // [MW_MAX_Q][MW_MAX_NODES] partial alignment sums
-    unsigned *ctr;   // [0] job sequence, [1] helper completions, [2] helper exits
+    unsigned *ctr;   // [0] job sequence; [32 (1 + s)] helper completions of shard s
+                     // (helper h -> shard h % MW_DONE_SHARDS); [32 (1 + MW_DONE_SHARDS)] exits
     int *err;        // set when a wait times out (the launch then ends early)
     int Q;
 };

@@ -76,7 +76,7 @@ __global__ __launch_bounds__(HPE_NT) void k_opt_init(DevOpt op, const double *__
     __syncthreads();
     const double c = eval_block<EV_COST, HPE_NT>(sm, o, cv, H, nullptr, pre);
     if (t == 0) op.pc[i] = c;
-    if (prep_arrive_last(op.ctr, (unsigned)op.P, &flag)) opt_update_gbest(op, sm, false, 0, true);
+    if (arrive_last_sharded(op.ctr, (unsigned)op.P, &flag)) opt_update_gbest(op, sm, false, 0, true);
 }
 
 // Descent phase of generation g (iter = g + 1).  Cloud (+ matchId) staged in LDS when
@@ -200,7 +200,7 @@ __global__ __launch_bounds__(RF_NT) void k_opt_descent(DevOpt op, const DevObs *
     // last workgroup: gbest <- particles.col(argmin pcost) if better (:643-650)
     Smem &sm = *reinterpret_cast<Smem *>(&rs);  // the refine workspace is dead here
     static_assert(sizeof(Smem) <= sizeof(RefineSm), "Smem overlay");
-    if (prep_arrive_last(op.ctr, (unsigned)op.P, &flag)) opt_update_gbest(op, sm, false, 0, false);
+    if (arrive_last_sharded(op.ctr, (unsigned)op.P, &flag)) opt_update_gbest(op, sm, false, 0, false);
 }
 
 // Velocity / position / cost phase of generation g.
@@ -237,5 +237,5 @@ __global__ __launch_bounds__(HPE_NT) void k_opt_move(DevOpt op, const DevObs *__
         if (t < HPE_DOF) op.pb[e] = xn;
         if (t == 0) op.pc[i] = fx;
     }
-    if (prep_arrive_last(op.ctr, (unsigned)op.P, &flag)) opt_update_gbest(op, sm, true, g, false);
+    if (arrive_last_sharded(op.ctr, (unsigned)op.P, &flag)) opt_update_gbest(op, sm, true, g, false);
 }

@@ -104,6 +104,38 @@ __device__ __forceinline__ bool prep_arrive_last(unsigned *ctr, unsigned parties
     return *flag != 0;
 }
 
+// The same for many arriving workgroups: one counter per shard (blockIdx % ARRIVE_SHARDS,
+// each on its own 128-B line) and a top counter the last of every shard increments, so
+// no address takes more than parties / ARRIVE_SHARDS + ARRIVE_SHARDS atomics (hundreds of
+// same-address atomics serialise at ~11-13 ns each).  ctr: ARRIVE_SHARDS * 32 + 1 words,
+// reset by the last arriver.
+#define ARRIVE_SHARDS 16
+__device__ __forceinline__ bool arrive_last_sharded(unsigned *ctr, unsigned parties, int *flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned s = blockIdx.x % ARRIVE_SHARDS;
+        const unsigned used = parties < ARRIVE_SHARDS ? parties : ARRIVE_SHARDS;
+        const unsigned size = parties / ARRIVE_SHARDS + (s < parties % ARRIVE_SHARDS ? 1u : 0u);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bool last = false;
+        if (atomicAdd(&ctr[s * 32], 1u) == size - 1) {  // last of its shard
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+            last = atomicAdd(&ctr[ARRIVE_SHARDS * 32], 1u) == used - 1;
+        }
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            for (int k = 0; k < ARRIVE_SHARDS; ++k) ctr[k * 32] = 0u;  // for the next launch
+            ctr[ARRIVE_SHARDS * 32] = 0u;
+        }
+        *flag = last ? 1 : 0;
+    }
+    __syncthreads();
+    return *flag != 0;
+}
+
 // ---- band workgroup b: rows [30b, 30b + 30)
 __device__ __forceinline__ void prep_band(const PrepArgs &a, int b, unsigned char *lds) {
     constexpr int W = HPE_IMG_W, NWV = PREP_NT / 64;

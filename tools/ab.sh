@@ -13,6 +13,6 @@ for r in $(seq 1 $R); do
     if [ -n "$EXTRA" ]; then
       HPE_LIB_VARIANT=$v timeout -k 10 200 python bench.py --steps 20 --no-cpu-baseline $EXTRA > gpurun_out/ab/benchx_$tag.log 2>&1 || exit 1
     fi
-    HPE_LIB_VARIANT=$v timeout -k 10 200 python tools/opt_time.py 32 100 1 > gpurun_out/ab/opt_$tag.log 2>&1 || exit 1
+    HPE_LIB_VARIANT=$v timeout -k 10 200 python tools/opt_time.py ${OPT_P:-32} 100 1 > gpurun_out/ab/opt_$tag.log 2>&1 || exit 1
   done
 done
