@@ -128,6 +128,23 @@ __device__ __forceinline__ void fk_wave_t(FkSm &f, const DevHand *__restrict__ H
     const int l = threadIdx.x & 63;
     StampClock sc;
     sc.start();
+    // hand constants of this lane's chain row and sphere items, loaded before the trig so
+    // their latency is not behind the phase fences
+    const int dl = (l < 15) ? l / 3 : 0;
+    const double L2 = H->L[dl][2], L3 = H->L[dl][3];
+    const double Fc = H->Fc[dl], Fs = H->Fs[dl], FLc = H->FLc[dl], FLs = H->FLs[dl];
+    const double T10x = H->T10x[dl], T10y = H->T10y[dl];
+    const double L1 = H->L[dl][1], tc = H->twc[dl], ts = H->tws[dl];
+    int sd[3], sa[3];
+    double swa[3], swb[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        const int it = l + 64 * q, s = (it < 3 * HPE_NS) ? it / 3 : 0;
+        sd[q] = H->dg[s];
+        sa[q] = H->ja[s];
+        swa[q] = H->wa[s];
+        swb[q] = H->wb[s];
+    }
     if (MODE != FK_TRANSLATE) {
         if (l < 23) {
             double a;
@@ -157,8 +174,6 @@ __device__ __forceinline__ void fk_wave_t(FkSm &f, const DevHand *__restrict__ H
             const double c2 = f.cs[4 + 4 * d], s2 = f.sn[4 + 4 * d];
             const double c3 = f.cs[5 + 4 * d], s3 = f.sn[5 + 4 * d];
             const double c4 = f.cs[6 + 4 * d], s4 = f.sn[6 + 4 * d];
-            const double L1 = H->L[d][1], L2 = H->L[d][2], L3 = H->L[d][3];
-            const double tc = H->twc[d], ts = H->tws[d];
             // Columns 0, 1, 3 of A*B with A = [[c1,0,-s1,0],[s1,0,c1,0],[0,-1,0,0]] and
             // B = [[c2,-s2*tc,s2*ts,L1*c2],[s2,c2*tc,-c2*ts,L1*s2],[0,ts,tc,0]]
             // (thumbmodel.cpp:144-153; fingers tc = 1, ts = 0, fingermodel.cpp:137-145).
@@ -182,11 +197,11 @@ __device__ __forceinline__ void fk_wave_t(FkSm &f, const DevHand *__restrict__ H
             const double g1 = q1 * cxr + q2 * sxr;
             const double g2 = q1 * (-sxr) + q2 * cxr;
             // cur1 = cur0 * F  (rotation about z + translation L0); its translation is X1 + u
-            const double h0 = g0 * H->Fc[d] + g1 * H->Fs[d];
-            const double h1 = g0 * (-H->Fs[d]) + g1 * H->Fc[d];
+            const double h0 = g0 * Fc + g1 * Fs;
+            const double h1 = g0 * (-Fs) + g1 * Fc;
             const double h2 = g2;
-            X1 = g0 * H->FLc[d] + g1 * H->FLs[d];
-            X0 = h0 * H->T10x[d] + h1 * H->T10y[d];  // (cur*T10) at i == 1
+            X1 = g0 * FLc + g1 * FLs;
+            X0 = h0 * T10x + h1 * T10y;  // (cur*T10) at i == 1
             // cur2 = cur1 * AB
             const double k0 = (h0 * AB00 + h1 * AB10) + h2 * AB20;
             const double k1 = (h0 * AB01 + h1 * AB11) + h2 * AB21;
@@ -222,8 +237,8 @@ __device__ __forceinline__ void fk_wave_t(FkSm &f, const DevHand *__restrict__ H
     for (int q = 0; q < 3; ++q) {
         const int it = l + 64 * q;
         if (it < 3 * HPE_NS) {
-            const int s = it / 3, r = it - 3 * (it / 3), d = H->dg[s], a = H->ja[s];
-            const double v = H->wa[s] * f.J[d][a][r] + H->wb[s] * f.J[d][a + 1][r];
+            const int s = it / 3, r = it - 3 * (it / 3), d = sd[q], a = sa[q];
+            const double v = swa[q] * f.J[d][a][r] + swb[q] * f.J[d][a + 1][r];
             const double vs = (r == 0) ? v : v * -1;
             f.S[s][r] = vs;
             f.Sp[r][s] = (float)vs;
