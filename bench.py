@@ -63,10 +63,13 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--seed", type=int, default=0, help="trajectory seed")
+    ap.add_argument("--frames", default=os.environ.get("HPE_FRAMES_DIR"),
+                    help="directory of MSRA-style *_depth.bin frames (headerless float32 mm, "
+                         "240x320) to track instead of the synthetic sequence")
     return ap.parse_args()
 
 
-def cpu_baseline(args, sizes_hint):
+def cpu_baseline(args, sizes_hint, recorded=None):
     """The oracle (C restatement, OpenMP over particles where the reference has
     `omp parallel for`) tracking the same synthetic frames on the host: a bounded
     sample of the same workload."""
@@ -84,8 +87,12 @@ def cpu_baseline(args, sizes_hint):
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
     P, G = args.particles, args.generations
     ub, lb, sd = hpe.reference_bounds()
-    poses = synth.trajectory(64, args.seed)
-    raw = [oracle_np.render_depth_mm(nh, poses[f]) for f in range(len(poses))]
+    if recorded is not None:  # the same recorded frames the GPU tracked
+        raw = recorded
+        poses = [hpe.X0.copy()]
+    else:
+        poses = synth.trajectory(64, args.seed)
+        raw = [oracle_np.render_depth_mm(nh, poses[f]) for f in range(len(poses))]
     x = poses[0].copy()
     done, t0, n_pts = 0, time.perf_counter(), 0
     while True:
@@ -168,8 +175,16 @@ def main():
     ds = not args.full_cloud
     # the input: raw 240x320 float32 mm depth frames in host memory, as load_data reads
     # them from .bin files (synthetic: rendered once from a seeded pose trajectory)
-    poses = synth.trajectory(n_frames, args.seed)
-    raw = [np.ascontiguousarray(ctx.render_depth(th)) for th in poses]
+    if args.frames:  # recorded frames, as load_data reads them (observedmodel.cpp:272-310)
+        files = sorted(Path(args.frames).glob("*_depth.bin"))
+        if len(files) < n_frames:
+            raise SystemExit(f"{args.frames}: {len(files)} *_depth.bin frames, need {n_frames}")
+        raw = [np.fromfile(fp, dtype="<f4", count=240 * 320).reshape(240, 320)
+               for fp in files[:n_frames]]
+        poses = None  # no ground truth: x0 of test_full (testmodel.cpp:38-40)
+    else:
+        poses = synth.trajectory(n_frames, args.seed)
+        raw = [np.ascontiguousarray(ctx.render_depth(th)) for th in poses]
     sizes = [len(hpe.preprocess_depth(d, True, ds)["cloud"]) for d in raw]
     NSLOT = 4  # frame slots in rotation: frame f+1 is prepared while frame f is tracked
     slot = (lambda f: f) if args.resident else (lambda f: f % NSLOT)
@@ -183,7 +198,7 @@ def main():
                                      0.7298, 1.49618, 1.49618, G + 1, 1e-8, 1e-8))
     ctx.check(lib.hpe_set_seed(ctx.h, C.c_uint64(subswarm_seed(rank))))
     state = torch.zeros(27, dtype=torch.float64, device=f"cuda:{local}")
-    state[:26] = torch.from_numpy(poses[0])
+    state[:26] = torch.from_numpy(poses[0] if poses is not None else hpe.X0.copy())
     torch.cuda.synchronize()
     ext = torch.cuda.ExternalStream(lib.hpe_stream(ctx.h), device=f"cuda:{local}")
     gathered = torch.zeros(world * 27, dtype=torch.float64, device=f"cuda:{local}")
@@ -240,6 +255,8 @@ def main():
         step(f)
         ctx.check(lib.hpe_sync(ctx.h))
         torch.cuda.synchronize()
+        if poses is None:
+            continue
         bp = state[:26].cpu().numpy()
         hand.build_hand_model(bp)
         est = hand.hand_joints.copy()
@@ -286,8 +303,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32+f64",
-        "data": "synthetic: seeded 26-DOF trajectory rendered from the 48-sphere model "
-                "into 240x320 float32 mm depth (no MSRA Subject1 on the box)",
+        "data": (f"recorded: {n_frames} *_depth.bin frames from {args.frames}" if args.frames else
+                 "synthetic: seeded 26-DOF trajectory rendered from the 48-sphere model "
+                 "into 240x320 float32 mm depth (no MSRA Subject1 on the box)"),
         "config": {"workload": ("tracked frame = " + ("" if args.resident else
                                 "next_frame preprocessing (GPU, fused into the refine launch) + ") +
                                 "refine_init_pose + pso_evolve + cal_cost(bestp)"),
@@ -296,10 +314,11 @@ def main():
                    "parallelism": f"subswarms x{world}, all-gather best per frame"},
         "tracked_fps": args.steps / el,
         "final_cost": float(final[26]),
-        "tracking_err_mm": {"sum_wrist_tips_mean": float(np.mean(errs)),
-                            "per_joint_mean": float(np.mean(errs) / 6),
-                            "note": "gnd_truth_err (costfunc.cpp:476-507) vs the synthetic "
-                                    "trajectory's true poses, second pass over the frames"},
+        "tracking_err_mm": ({"sum_wrist_tips_mean": float(np.mean(errs)),
+                             "per_joint_mean": float(np.mean(errs) / 6),
+                             "note": "gnd_truth_err (costfunc.cpp:476-507) vs the synthetic "
+                                     "trajectory's true poses, second pass over the frames"}
+                            if errs else None),
         "roofline": {
             "bound": "hbm", "kernel": "k_pso_gen",
             "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -318,7 +337,7 @@ def main():
         "host_us_per_step": host_s / args.steps * 1e6,
     }
     if world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args, sizes)
+        line["cpu_baseline"] = cpu_baseline(args, sizes, raw if args.frames else None)
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
