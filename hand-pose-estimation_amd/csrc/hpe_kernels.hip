@@ -561,14 +561,20 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
 // Last end-of-generation update and bestp = gbest_pos (PSO.cpp:864-882).  Replays the
 // gbest / count sequence from gmin[], finds the last improving generation g* and takes
 // particles.col(first argmin pcost) of that generation; resets gmin[] for the next call.
-// TAIL (a tracked frame, testmodel.cpp:130-132): the same block then evaluates
-// cal_cost(bestp) into out[26] -- eval_block as in k_eval, so the same bits -- and copies
-// the frame descriptor it used to obs_out (the API's "selected frame").
+// TAIL (a tracked frame, testmodel.cpp:130-132): out[26] = cal_cost(bestp), and the
+// frame descriptor used is copied to obs_out (the API's "selected frame").  When some
+// generation improved, bestp = particles.col(argmin pcost) of the last improving
+// generation g*, and that particle's pbest cost was set AT g* (an older value could not
+// undercut the previous gbest), i.e. it IS cal_cost(bestp) computed by the same
+// eval_block on the same theta: the gbest cost is kept, bit for bit (same_eval: the
+// generations used the workgroup form).  Otherwise (nothing beat 1e100, bestp = zeros)
+// the block evaluates it.
 template <bool TAIL = false>
 __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__restrict__ out,
                                                       const DevObs *__restrict__ og = nullptr,
                                                       const DevHand *__restrict__ Hg = nullptr,
-                                                      DevObs *__restrict__ obs_out = nullptr) {
+                                                      DevObs *__restrict__ obs_out = nullptr,
+                                                      int same_eval = 0) {
     constexpr int CH = 2048;  // generations staged per pass
     __shared__ Smem sm;
     __shared__ double gm[CH];
@@ -642,10 +648,11 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
     if (t < HPE_DOF) sw.gpos[t] = out[t];
     for (int c = t; c < (G + 1) * GMIN_SHARDS; c += HPE_NT) sw.gmin[(size_t)c * GMIN_STRIDE] = ~0ull;
     if (TAIL) {
-        const DevObs o = *og;
-        if (t < HPE_DOF) sm.fk.th[t] = out[t];
         if (obs_out && t < (int)(sizeof(DevObs) / 8))
             ((unsigned long long *)obs_out)[t] = ((const unsigned long long *)og)[t];
+        if (same_eval && last >= 0) return;  // out[26] = gcost = cal_cost(bestp)
+        const DevObs o = *og;
+        if (t < HPE_DOF) sm.fk.th[t] = out[t];
         const CloudView cv = obs_cloud(o);
         const Pt pre = load_pt(cv, t);
         __syncthreads();
