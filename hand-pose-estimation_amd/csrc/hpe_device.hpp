@@ -31,6 +31,23 @@ __device__ unsigned long long hpe_stamps[64];
 #define HPE_GOLD_LOG 65536
 __device__ unsigned long long hpe_gold_log[1 + HPE_GOLD_LOG];  // [0] = count
 #endif
+// Per-block wall-clock stamps of k_pso_gen (100 MHz s_memrealtime, comparable across CUs):
+// [generation][block][point], written by thread 0 (diagnostic build only).
+#define BT_GENS 48
+#define BT_BLK 256
+#define BT_PTS 8
+#if HPE_STAMPS
+__device__ unsigned long long hpe_blk_ts[BT_GENS * BT_BLK * BT_PTS];
+#define BLK_TS(g, k)                                                                       \
+    do {                                                                                   \
+        if (threadIdx.x == 0 && (g) < BT_GENS && blockIdx.x < BT_BLK)                      \
+            hpe_blk_ts[((g) * BT_BLK + blockIdx.x) * BT_PTS + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define BLK_TS(g, k) \
+    do {             \
+    } while (0)
+#endif
 struct StampClock {
     unsigned long long t, t0 = 0, r0 = 0;
     // whole-kernel span of block 0: shader cycles into slot k, 100 MHz ticks into k + 1
@@ -81,18 +98,43 @@ struct __align__(16) Smem {
     double draws[2 * HPE_DOF];  // rp, rg of the generation (k_pso_gen)
 };
 
-// Cloud + correspondences, either in LDS (staged) or in HBM.
-struct CloudView {
-    const double *cx, *cy, *cz;
+// Global-memory pointers.  Pointers read from memory (the frame descriptor DevObs) are
+// generic to the compiler, so their loads become flat_load, which count on BOTH vmcnt and
+// lgkmcnt: every later LDS or scalar-load wait then also waits for the HBM round trip.
+// Loading through an address_space(1) pointer gives global_load (vmcnt only).
+#define HPE_GAS __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ const HPE_GAS T *gp(const T *p) {
+    return (const HPE_GAS T *)p;
+}
+
+// Cloud + correspondences, either in LDS (staged; generic pointers into a __shared__
+// array, whose address space the compiler infers) or in HBM (CloudGlobal).
+template <class P>
+struct CloudT {
+    P cx, cy, cz;
     int n;
 };
+using CloudView = CloudT<const double *>;
+using CloudGlobal = CloudT<const HPE_GAS double *>;
 
-// Copy the hand constants into LDS; caller synchronises before use.
+// Copy the hand constants into LDS in two halves: hand_word() issues this thread's load
+// (unconditional, so no branch forces an early wait), hand_put() stores it once the
+// caller has issued its other loads; the caller synchronises before use.
+template <int NT>
+__device__ __forceinline__ double hand_word(const DevHand *__restrict__ src) {
+    constexpr int NWD = (int)(sizeof(DevHand) / 8);
+    static_assert(sizeof(DevHand) % 8 == 0 && NWD <= NT, "one 8-byte hand word per thread");
+    const int q = threadIdx.x < NWD ? threadIdx.x : NWD - 1;
+    return gp((const double *)src)[q];
+}
+template <int NT>
+__device__ __forceinline__ void hand_put(DevHand &dst, double v) {
+    if (threadIdx.x < (int)(sizeof(DevHand) / 8)) ((double *)&dst)[threadIdx.x] = v;
+}
 template <int NT>
 __device__ __forceinline__ void stage_hand(DevHand &dst, const DevHand *__restrict__ src) {
-    static_assert(sizeof(DevHand) % 8 == 0, "DevHand must be a multiple of 8 bytes");
-    for (int q = threadIdx.x; q < (int)(sizeof(DevHand) / 8); q += NT)
-        ((double *)&dst)[q] = ((const double *)src)[q];
+    hand_put<NT>(dst, hand_word<NT>(src));
 }
 
 __device__ __forceinline__ void wave_sync() {
@@ -355,27 +397,46 @@ __device__ __forceinline__ void block_sum3(double (*red)[4], double &a, double &
 
 // ---------------------------------------------------------------- cost terms
 // depth_penalty term of sphere i (costfunc.cpp:249-300); S is un-negated on the fly.
-__device__ __forceinline__ double depth_term(const FkSm &f, int i, const DevObs &o,
-                                             const DevHand *__restrict__ H) {
+// Two halves, so that the gathers' L2 round trip overlaps the caller's other work:
+//   depth_issue  projection + BOTH gathers (depth and DT at a clamped pixel), issued
+//                unconditionally by every lane (sphere index clamped);
+//   depth_finish waits for them (an empty asm consumes the loaded registers, so the
+//                compiler can neither wait earlier nor sink a load into the reference's
+//                branches) and evaluates the branches as selects; 0 where !use.
+struct DepthG {
+    double djc, z, r;
+    float dtp;
+    bool in;
+};
+__device__ __forceinline__ DepthG depth_issue(const FkSm &f, int i, const DevObs &o,
+                                              const DevHand *__restrict__ H) {
+    i = i < HPE_NS ? i : HPE_NS - 1;
     const double x = f.S[i][0], y = f.S[i][1] * -1, z = f.S[i][2] * -1;
     const double pu = (o.K[0] * x + o.K[1] * y) + o.K[2] * z;
     const double pv = (o.K[3] * x + o.K[4] * y) + o.K[5] * z;
     const double pw = (o.K[6] * x + o.K[7] * y) + o.K[8] * z;
     const double dx = floor(pu / pw), dy = floor(pv / pw);
-    const double r = H->radii[i];
-    if (dx >= 0 && dx < HPE_IMG_W && dy >= 0 && dy < HPE_IMG_H) {
-        const int pix = (int)dy * HPE_IMG_W + (int)dx;
-        const double djc = o.depth[pix];
-        if (djc != 0.0) {
-            const double tt = djc - z;
-            const double diff = (0.0 < tt) ? tt : 0.0;  // std::max(0.0, tt)
-            return diff * diff;
-        }
-        const double dd = (double)o.dt[pix] * o.scale + r;
-        return dd * dd;
-    }
-    const double md = o.dtmax * o.scale + r;
-    return md * md;
+    DepthG d;
+    d.in = dx >= 0 && dx < HPE_IMG_W && dy >= 0 && dy < HPE_IMG_H;  // NaN: off-image
+    const int pix = d.in ? (int)dy * HPE_IMG_W + (int)dx : 0;
+    d.djc = gp(o.depth)[pix];
+    d.dtp = gp(o.dt)[pix];
+    d.z = z;
+    d.r = H->radii[i];
+    return d;
+}
+__device__ __forceinline__ double depth_finish(DepthG d, const DevObs &o, bool use) {
+    asm volatile("" : "+v"(d.djc), "+v"(d.dtp));
+    const double tt = d.djc - d.z;
+    const double diff = (0.0 < tt) ? tt : 0.0;  // std::max(0.0, tt)
+    const double dd = (double)d.dtp * o.scale + d.r;
+    const double md = o.dtmax * o.scale + d.r;  // off-image: max of the DT (:298)
+    const double v = !d.in ? md * md : (d.djc != 0.0) ? diff * diff : dd * dd;
+    return use ? v : 0.0;
+}
+__device__ __forceinline__ double depth_term(const FkSm &f, int i, const DevObs &o,
+                                             const DevHand *__restrict__ H) {
+    return depth_finish(depth_issue(f, i, o, H), o, true);
 }
 
 // one of the 144 self-collision pairs (costfunc.cpp:150-193)
@@ -420,7 +481,8 @@ __device__ __forceinline__ int sqrt_class_key(int hb, float d2) {
 struct Pt {
     double x, y, z;
 };
-__device__ __forceinline__ Pt load_pt(const CloudView &cv, int it) {
+template <class CV>
+__device__ __forceinline__ Pt load_pt(const CV &cv, int it) {
     const int p = it >> 1;
     if (it < 2 * cv.n) return Pt{cv.cx[p], cv.cy[p], cv.cz[p]};
     return Pt{0, 0, 0};
@@ -428,8 +490,8 @@ __device__ __forceinline__ Pt load_pt(const CloudView &cv, int it) {
 // pre: the point of item threadIdx.x, loaded early by the caller (load_pt) so its
 // latency hides under FK.
 // gt: this thread's index among the NT threads searching for the particle.
-template <int NT, bool STORE_MATCH>
-__device__ __forceinline__ double search_align(const FkSm &f, const CloudView &cv,
+template <int NT, bool STORE_MATCH, class CV>
+__device__ __forceinline__ double search_align(const FkSm &f, const CV &cv,
                                                const DevHand *__restrict__ H,
                                                int32_t *__restrict__ match, Pt pre,
                                                int gt = -1) {
@@ -488,7 +550,8 @@ __device__ __forceinline__ double search_align(const FkSm &f, const CloudView &c
 
 // Alignment with frozen correspondences (cal_cost2(..., compute_corr=false)) over
 // `stride` lanes starting at `lane0`; four points in flight per lane.
-__device__ __forceinline__ double align_one(const FkSm &f, const CloudView &cv,
+template <class CV>
+__device__ __forceinline__ double align_one(const FkSm &f, const CV &cv,
                                             const DevHand *__restrict__ H,
                                             const int32_t *__restrict__ match, int p) {
     const int idx = match[p];
@@ -497,7 +560,8 @@ __device__ __forceinline__ double align_one(const FkSm &f, const CloudView &cv,
     const double e = sqrt((dx * dx + dy * dy) + dz * dz) - H->radii[idx];
     return e * e;
 }
-__device__ __forceinline__ double align_frozen(const FkSm &f, const CloudView &cv,
+template <class CV>
+__device__ __forceinline__ double align_frozen(const FkSm &f, const CV &cv,
                                                const DevHand *__restrict__ H,
                                                const int32_t *__restrict__ match, int lane0,
                                                int stride) {
@@ -523,27 +587,29 @@ enum EvalMode { EV_COST = 0, EV_COST2_CORR = 1, EV_COST2_FROZEN = 2, EV_COST_STO
 // cal_cost of the particle in f.th by ONE wave (FK + search over 64 lanes): the
 // throughput form used when there are many more particles than CUs.  All lanes return
 // the total; pre = load_pt(cv, lane).
-__device__ __forceinline__ double eval_wave_cost(FkSm &f, const DevObs &o, const CloudView &cv,
+template <class CV>
+__device__ __forceinline__ double eval_wave_cost(FkSm &f, const DevObs &o, const CV &cv,
                                                  const DevHand *__restrict__ H, Pt pre) {
     const int l = threadIdx.x & 63;
     fk_wave(f, H);
-    double dep = (l < HPE_NS) ? depth_term(f, l, o, H) : 0.0;
+    const DepthG dg = depth_issue(f, l, o, H);
     double al = search_align<64, false>(f, cv, H, nullptr, pre, l);
+    double dep = depth_finish(dg, o, l < HPE_NS);
     double co = 0.0;
     wave_sum3(al, dep, co);
     return al * o.lambda + dep;
 }
 
-__device__ __forceinline__ CloudView obs_cloud(const DevObs &o) {
-    return CloudView{o.cx, o.cy, o.cz, o.n};
+__device__ __forceinline__ CloudGlobal obs_cloud(const DevObs &o) {
+    return CloudGlobal{gp(o.cx), gp(o.cy), gp(o.cz), o.n};
 }
 
 // Whole-block evaluation of the particle in sm.fk.th (wave 0 does FK, NT threads the
 // search).  Every thread returns the total; terms (align, depth, collision) go to
 // sm.dscal[0..2].
 // FK = false: the caller has already placed the centres in sm.fk.S / Sp (hpe_eval_spheres).
-template <int MODE, int NT, bool FK = true>
-__device__ __forceinline__ double eval_block(Smem &sm, const DevObs &o, const CloudView &cv,
+template <int MODE, int NT, bool FK = true, class CV>
+__device__ __forceinline__ double eval_block(Smem &sm, const DevObs &o, const CV &cv,
                                              const DevHand *__restrict__ H,
                                              int32_t *__restrict__ match, Pt pre) {
     StampClock sc;
@@ -555,7 +621,7 @@ __device__ __forceinline__ double eval_block(Smem &sm, const DevObs &o, const Cl
     sc.lap(10);
     const int t = threadIdx.x;
     // issue the depth gathers first: their latency hides under the search
-    double dep = (t < HPE_NS) ? depth_term(sm.fk, t, o, H) : 0.0;
+    const DepthG dg = depth_issue(sm.fk, t, o, H);
     double al;
     if (MODE == EV_COST2_FROZEN) al = align_frozen(sm.fk, cv, H, match, t, NT);
     else if (MODE == EV_COST2_CORR || MODE == EV_COST_STORE)
@@ -563,6 +629,7 @@ __device__ __forceinline__ double eval_block(Smem &sm, const DevObs &o, const Cl
     else al = search_align<NT, false>(sm.fk, cv, H, nullptr, pre);
     const bool coll = (MODE == EV_COST2_CORR || MODE == EV_COST2_FROZEN);
     double co = (coll && t < 144) ? collide_term(sm.fk, t, H) : 0.0;
+    double dep = depth_finish(dg, o, t < HPE_NS);
     sc.lap(11);
     block_sum3<NT, false, !(MODE == EV_COST2_CORR || MODE == EV_COST2_FROZEN)>(sm.red, al, dep, co);
     sc.lap(12);
@@ -581,8 +648,9 @@ __device__ __forceinline__ double eval_block(Smem &sm, const DevObs &o, const Cl
 // the total.
 // Xt != nullptr: f.th differs from the theta of Xt only in the global position
 // (FK_TRANSLATE).
+template <class CV>
 __device__ __forceinline__ double eval_wave_frozen(FkSm &f, const DevObs &o,
-                                                   const CloudView &cv,
+                                                   const CV &cv,
                                                    const DevHand *__restrict__ H,
                                                    const int32_t *__restrict__ match,
                                                    FkX *Xt = nullptr) {
@@ -591,12 +659,13 @@ __device__ __forceinline__ double eval_wave_frozen(FkSm &f, const DevObs &o,
     StampClock sc;
     sc.start();
     const int l = threadIdx.x & 63;
-    double dep = (l < HPE_NS) ? depth_term(f, l, o, H) : 0.0;
+    const DepthG dg = depth_issue(f, l, o, H);
     sc.lap(15);
     double al = align_frozen(f, cv, H, match, l, 64);
     sc.lap(16);
     double co = collide_term(f, l, H) + collide_term(f, l + 64, H) +
                 ((l < 16) ? collide_term(f, l + 128, H) : 0.0);
+    double dep = depth_finish(dg, o, l < HPE_NS);
     sc.lap(17);
     wave_sum3(al, dep, co);
     sc.lap(18);

@@ -12,6 +12,8 @@
 //
 // One workgroup of HPE_NT threads per particle; see hpe_device.hpp for the block-level
 // pieces and DESIGN.md for layout, rooflines and the parity argument.
+#include <vector>
+
 #include "hpe_device.hpp"
 #include "hpe_prep.hpp"
 #include "../../include/hpe.h"
@@ -54,7 +56,7 @@ __global__ __launch_bounds__(HPE_NT) void k_eval(const double *__restrict__ thet
     stage_hand<HPE_NT>(sm.hand, Hg);
     const DevHand *__restrict__ H = &sm.hand;
     if (t < HPE_DOF) sm.fk.th[t] = theta[(size_t)i * HPE_DOF + t];
-    const CloudView cv = obs_cloud(o);
+    const CloudGlobal cv = obs_cloud(o);
     const Pt pre = load_pt(cv, t);
     __syncthreads();
     int32_t *m = match ? match + (size_t)i * o.n : nullptr;
@@ -88,7 +90,7 @@ __global__ __launch_bounds__(HPE_NT) void k_eval_spheres(const double *__restric
         sm.fk.S[s][r] = v;
         sm.fk.Sp[r][s] = (float)v;
     }
-    const CloudView cv = obs_cloud(o);
+    const CloudGlobal cv = obs_cloud(o);
     const Pt pre = load_pt(cv, t);
     __syncthreads();
     eval_block<MODE, HPE_NT, false>(sm, o, cv, H, match + (size_t)i * o.n, pre);
@@ -154,16 +156,24 @@ __device__ __forceinline__ unsigned long long *gmin_cell(const DevSwarm &sw, int
 __device__ __forceinline__ void gmin_lower(const DevSwarm &sw, int g, int i, double c) {
     atomicMin(gmin_cell(sw, g, i % GMIN_SHARDS), f64_to_bits(c));
 }
-// min over generation g's shards by one whole wave, in every lane; NaN if none was written
-__device__ __forceinline__ double gmin_read(const DevSwarm &sw, int g) {
+// min over generation g's shards by one whole wave, in every lane; NaN if none was written.
+// gmin_load issues lane l's cell (unconditional), gmin_reduce folds the wave.
+__device__ __forceinline__ unsigned long long gmin_load(const DevSwarm &sw, int g) {
     const int l = threadIdx.x & 63;
-    double m = (l < GMIN_SHARDS) ? bits_to_f64(*gmin_cell(sw, g, l)) : __builtin_nan("");
+    return *gmin_cell(sw, g, l < GMIN_SHARDS ? l : 0);
+}
+__device__ __forceinline__ double gmin_reduce(unsigned long long cell) {
+    const int l = threadIdx.x & 63;
+    double m = (l < GMIN_SHARDS) ? bits_to_f64(cell) : __builtin_nan("");
     m = fmin(m, dpp_f64<0xB1>(m));
     m = fmin(m, dpp_f64<0x4E>(m));
     m = fmin(m, dpp_f64<0x141>(m));
     m = fmin(m, dpp_f64<0x140>(m));
     return fmin(fmin(readlane_f64(m, 0), readlane_f64(m, 16)),
                 fmin(readlane_f64(m, 32), readlane_f64(m, 48)));
+}
+__device__ __forceinline__ double gmin_read(const DevSwarm &sw, int g) {
+    return gmin_reduce(gmin_load(sw, g));
 }
 
 __device__ __forceinline__ size_t ib_index(const DevSwarm &sw, int par, int var, int r, int slot) {
@@ -185,15 +195,24 @@ __device__ __forceinline__ void push_inbox(const DevSwarm &sw, int g, int s, int
     sw.inbox[ib_index(sw, g & 1, var, r, slot) + fld] = val;
 }
 
-// Link of lane q of the pushing waves for topology tt (r = -1 when nothing is pushed).
-__device__ __forceinline__ void load_link(const DevSwarm &sw, int g, int s, int q, int tt, int &r,
-                                          int &slot) {
-    r = -1;
-    slot = 0;
-    if (g >= sw.G || q >= 6 * IB_FIELDS || tt < 1) return;
-    const int *o = sw.outl + (((size_t)tt * sw.P + s) * 3 + (q / IB_FIELDS) % 3) * 2;
-    r = o[0];
-    slot = o[1];
+// Link of lane q of the pushing waves for topology tt: {receiver, slot} as one 8-byte
+// load.  Loaded unconditionally (a lane with nothing to push reads entry 0 and is marked
+// !ok), so no branch merge makes the wave wait for it before its use at the push.
+struct Link {
+    long long raw;
+    bool ok;
+};
+__device__ __forceinline__ Link load_link(const DevSwarm &sw, int g, int s, int q, int tt,
+                                          bool want = true) {
+    Link L;
+    L.ok = want && g < sw.G && q >= 0 && q < 6 * IB_FIELDS && tt >= 1;
+    const size_t k = L.ok ? ((size_t)tt * sw.P + s) * 3 + (q / IB_FIELDS) % 3 : 0;
+    L.raw = ((const long long *)sw.outl)[k];
+    return L;
+}
+__device__ __forceinline__ void push_inbox(const DevSwarm &sw, int g, int s, int q, const Link &L,
+                                           int tt, double pc, const double *row) {
+    push_inbox(sw, g, s, q, L.ok ? (int)(L.raw & 0xffffffff) : -1, (int)(L.raw >> 32), tt, pc, row);
 }
 
 __global__ __launch_bounds__(HPE_NT) void k_pso_init(DevSwarm sw, const double *__restrict__ x0,
@@ -201,13 +220,14 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_init(DevSwarm sw, const double *
     const DevObs o = *og;  // the selected frame (device-resident: graph-stable args)
     __shared__ Smem sm;
     const int i = blockIdx.x, t = threadIdx.x;
-    stage_hand<HPE_NT>(sm.hand, Hg);
+    const double hw = hand_word<HPE_NT>(Hg);
     const DevHand *__restrict__ H = &sm.hand;
     const double *sd = sw.bounds + 2 * HPE_DOF;
-    int lr, ls;  // pushing lanes: waves 1..3 (q = t - 64), topology 1 = rebuilt for gen 1
+    // pushing lanes: waves 1..3 (q = t - 64), topology 1 = rebuilt for gen 1
     const int q = t - 64;
-    if (q >= 0 && q < 3 * IB_FIELDS) load_link(sw, 0, i, q, 1, lr, ls);
-    else lr = -1, ls = 0;
+    const Link lk = load_link(sw, 0, i, q, 1, q < 3 * IB_FIELDS);
+    const CloudGlobal cv = obs_cloud(o);
+    const Pt pre = load_pt(cv, t);
     if (t < HPE_DOF) {  // particles = x0 + randn % std (PSO.cpp:67-72)
         const size_t e = (size_t)i * HPE_DOF + t;
         const double x = x0[t] + sw.normals[e] * sd[t];
@@ -216,15 +236,14 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_init(DevSwarm sw, const double *
         sw.pb[e] = x;
         sw.v[e] = 0.0;
     }
-    const CloudView cv = obs_cloud(o);
-    const Pt pre = load_pt(cv, t);
+    hand_put<HPE_NT>(sm.hand, hw);
     __syncthreads();
     const double c = eval_block<EV_COST, HPE_NT>(sm, o, cv, H, nullptr, pre);
     if (t == 0) {  // PSO.cpp:748-763; pbest costs are >= 0, so their bits order like values
         sw.pch[i] = c;
         gmin_lower(sw, 0, i, c);
     }
-    push_inbox(sw, 0, i, q, lr, ls, 1, c, sm.fk.th);
+    push_inbox(sw, 0, i, q, lk, 1, c, sm.fk.th);
 }
 
 // One fused generation g >= 1 (PSO.cpp:781-879).  Wave 0 carries the serial part: every
@@ -234,38 +253,42 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_init(DevSwarm sw, const double *
 __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *__restrict__ og,
                                                     const DevHand *__restrict__ Hg, int g,
                                                     double W1, double C1, double C2) {
+    BLK_TS(g, 0);
     StampClock sc;
     sc.begin();
     const DevObs o = *og;  // the selected frame (device-resident: graph-stable args)
     __shared__ Smem sm;
     __shared__ double ib[2][IB_KMAX][IB_FIELDS];
     const int i = blockIdx.x, t = threadIdx.x, P = sw.P, K = sw.K;
-    stage_hand<HPE_NT>(sm.hand, Hg);
+    // Round 1: every load of the generation is issued before any value is used (one
+    // memory round trip): hand words, first cloud point, push links, inbox payload rows
+    // (waves 1..7); own state, own pbest cost, inbox tags / costs, gmin cells, sig (wave 0).
+    const double hw = hand_word<HPE_NT>(Hg);  // staged into LDS before the first barrier
     const DevHand *__restrict__ H = &sm.hand;
     sc.lap(4);
-    const CloudView cv = obs_cloud(o);
+    const CloudGlobal cv = obs_cloud(o);
     const Pt pre = load_pt(cv, t);  // this thread's first cloud point, used after FK
     const size_t e = (size_t)i * HPE_DOF + t;
     const int q = t - 64;  // pushing lanes (waves 1..3): var-1 links now, var-0 after the decision
-    int lr = -1, ls = 0;
-    if (q >= 0 && q < 3 * IB_FIELDS) load_link(sw, g, i, q, g + 1, lr, ls);
+    const Link lk1 = load_link(sw, g, i, q, g + 1, q < 3 * IB_FIELDS);
     double pbi = 0, xo = 0, vo = 0, rp = 0, rg = 0;  // own state (lanes t < 26 of wave 0)
+    double lbt = 0, ubt = 0;                          // bounds of dimension t
     int inf = 0, islot = -1, var = 0;
-    if (t >= 64 && t < 64 + 2 * HPE_DOF) {  // wave 1 draws rp, rg while wave 0 waits on loads
-        const int j = t - 64, d = j < HPE_DOF ? j : j - HPE_DOF;
-        sm.draws[j] = philox_u01(sw.seed, j < HPE_DOF ? ST_RP : ST_RG, g, i, d);
-    }
     if (t >= 64) {
-        // ---- waves 1..7: both informant inboxes (payload rows) into LDS, loads first
+        // ---- waves 1..7: both informant inboxes (payload rows) into LDS
         const double *src = sw.inbox + ib_index(sw, (g - 1) & 1, 0, i, 0);
         const size_t var_stride = (size_t)P * K * IB_FIELDS;
         const int n = 2 * K * IB_FIELDS, u0 = t - 64;
         double a[3];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const int u = u0 + k * (HPE_NT - 64);
+        for (int k = 0; k < 3; ++k) {  // unconditional (clamped) loads: no early wait
+            const int u = min(u0 + k * (HPE_NT - 64), n - 1);
             const int vr = u >= K * IB_FIELDS ? 1 : 0;
-            a[k] = (u < n) ? src[vr * var_stride + (u - vr * K * IB_FIELDS)] : 0.0;
+            a[k] = src[vr * var_stride + (u - vr * K * IB_FIELDS)];
+        }
+        if (t < 64 + 2 * HPE_DOF) {  // wave 1 draws rp, rg while the loads are in flight
+            const int j = t - 64, d = j < HPE_DOF ? j : j - HPE_DOF;
+            sm.draws[j] = philox_u01(sw.seed, j < HPE_DOF ? ST_RP : ST_RG, g, i, d);
         }
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -273,24 +296,24 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
             if (u < n) (&ib[0][0][0])[(u >= K * IB_FIELDS ? IB_KMAX * IB_FIELDS - K * IB_FIELDS : 0) + u] = a[k];
         }
     } else {
-        // ---- wave 0, round 1: own state, draws, gbest bookkeeping, inbox tags / costs
-        if (t < HPE_DOF) {
-            xo = sw.xh[(size_t)(g - 1) * P * HPE_DOF + e];
-            vo = sw.v[e];
-            pbi = sw.pb[e];
-        }
+        // ---- wave 0, round 1: own state, gbest bookkeeping, inbox tags / costs
+        const size_t ec = (size_t)i * HPE_DOF + (t < HPE_DOF ? t : HPE_DOF - 1);
+        xo = sw.xh[(size_t)(g - 1) * P * HPE_DOF + ec];
+        vo = sw.v[ec];
+        pbi = sw.pb[ec];
+        lbt = sw.bounds[ec - (size_t)i * HPE_DOF];
+        ubt = sw.bounds[ec - (size_t)i * HPE_DOF + HPE_DOF];
         const double pci = sw.pch[(size_t)(g - 1) * P + i];  // own pbest cost (uniform)
-        const double fmin = gmin_read(sw, g - 1);  // NaN when no value was written
-        const Sig pv = sw.sig[g > 1 ? g - 1 : 0];
-        double tg[2] = {0, 0}, tc[2] = {0, 0};
-        if (t < K) {
+        double tg[2], tc[2];
 #pragma unroll
-            for (int vr = 0; vr < 2; ++vr) {
-                const double *sl = sw.inbox + ib_index(sw, (g - 1) & 1, vr, i, t);
-                tg[vr] = sl[0];
-                tc[vr] = sl[1];
-            }
+        for (int vr = 0; vr < 2; ++vr) {
+            const double *sl = sw.inbox + ib_index(sw, (g - 1) & 1, vr, i, t < K ? t : K - 1);
+            tg[vr] = sl[0];
+            tc[vr] = sl[1];
         }
+        const unsigned long long gcell = gmin_load(sw, g - 1);
+        const Sig pv = sw.sig[g > 1 ? g - 1 : 0];
+        const double fmin = gmin_reduce(gcell);  // NaN when no value was written
         // end-of-generation update of g-1 (PSO.cpp:864-877) / initial gbest (:755-760),
         // computed redundantly by every lane (uniform values)
         Sig sg;
@@ -331,13 +354,15 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
         wave_argmin_lex(v, idx, slot, inf, islot);
         sc.lap(1);
     }
+    hand_put<HPE_NT>(sm.hand, hw);
+    BLK_TS(g, 1);
     __syncthreads();  // informant rows and draws in LDS
+    BLK_TS(g, 2);
     if (t < 64) {
         // ---- velocity, position, check_constraints (PSO.cpp:824-842, 358-377)
         if (t < HPE_DOF) {
             rp = sm.draws[t];
             rg = sm.draws[HPE_DOF + t];
-            const double *lb = sw.bounds, *ub = sw.bounds + HPE_DOF;
             double vn;
             if (inf == i) {
                 vn = W1 * vo + (C1 * rp) * (pbi - xo);
@@ -347,8 +372,8 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
             }
             double xn = xo + vn;
             const double xr = xn;
-            if (xr < lb[t]) { xn = lb[t]; vn = 0.; }
-            if (xr > ub[t]) { xn = lb[t]; vn = 0.; }  // above max -> MIN (PSO.cpp:372)
+            if (xr < lbt) { xn = lbt; vn = 0.; }
+            if (xr > ubt) { xn = lbt; vn = 0.; }  // above max -> MIN (PSO.cpp:372)
             sw.v[e] = vn;
             sw.xh[(size_t)g * P * HPE_DOF + e] = xn;
             sm.fk.th[t] = xn;
@@ -358,11 +383,13 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
         fk_wave(sm.fk, H);
     }
     __syncthreads();  // spheres, topology and own pbest cost published
+    BLK_TS(g, 3);
     const int topo = sm.iscal[0];
     const double pci = sm.dscal[4];
-    if (q >= 3 * IB_FIELDS && q < 6 * IB_FIELDS) load_link(sw, g, i, q, topo, lr, ls);
+    const Link lk0 = load_link(sw, g, i, q, topo, q >= 3 * IB_FIELDS);
     // ---- evaluation and pbest (PSO.cpp:848-861)
     const double fx = eval_block<EV_COST, HPE_NT, false>(sm, o, cv, H, nullptr, pre);
+    BLK_TS(g, 4);
     sc.start();
     const bool better = fx < pci;
     const double pn = better ? fx : pci;
@@ -376,7 +403,8 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
         gmin_lower(sw, g, i, pn);
     }
     __syncthreads();
-    push_inbox(sw, g, i, q, lr, ls, q < 3 * IB_FIELDS ? g + 1 : topo, pn, sm.fk.th);
+    push_inbox(sw, g, i, q, q < 3 * IB_FIELDS ? lk1 : lk0, q < 3 * IB_FIELDS ? g + 1 : topo, pn, sm.fk.th);
+    BLK_TS(g, 5);
     sc.lap(3);
     sc.span(5);
 }
@@ -391,12 +419,12 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
 #define PW_NT (64 * PW_WPB)
 
 __device__ __forceinline__ void push_lane_links(const DevSwarm &sw, int g, int i, int l, int tt0,
-                                                int tt1, int (&lr)[3], int (&ls)[3]) {
+                                                int tt1, Link (&lk)[3]) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const int q = l + 64 * k;
         const int tt = (q < 3 * IB_FIELDS) ? tt0 : tt1;
-        load_link(sw, g, i, q, tt, lr[k], ls[k]);
+        lk[k] = load_link(sw, g, i, q, tt);
     }
 }
 
@@ -410,12 +438,12 @@ __global__ __launch_bounds__(PW_NT) void k_pso_init_w(DevSwarm sw, const double 
     const int i = blockIdx.x * PW_WPB + w, P = sw.P;
     const bool valid = i < P;
     const int ic = valid ? i : P - 1;
-    stage_hand<PW_NT>(hs, Hg);
+    const double hw = hand_word<PW_NT>(Hg);
     const DevHand *__restrict__ H = &hs;
     FkSm &f = fks[w];
-    int lr[3], ls[3];
-    push_lane_links(sw, 0, ic, l, 1, -1, lr, ls);
-    const CloudView cv = obs_cloud(o);
+    Link lk[3];
+    push_lane_links(sw, 0, ic, l, 1, -1, lk);
+    const CloudGlobal cv = obs_cloud(o);
     const Pt pre = load_pt(cv, l);
     const double *sd = sw.bounds + 2 * HPE_DOF;
     if (l < HPE_DOF) {  // particles = x0 + randn % std (PSO.cpp:67-72)
@@ -428,6 +456,7 @@ __global__ __launch_bounds__(PW_NT) void k_pso_init_w(DevSwarm sw, const double 
             sw.v[e] = 0.0;
         }
     }
+    hand_put<PW_NT>(hs, hw);
     __syncthreads();  // hand staged
     const double c = eval_wave_cost(f, o, cv, H, pre);
     if (!valid) return;
@@ -436,7 +465,7 @@ __global__ __launch_bounds__(PW_NT) void k_pso_init_w(DevSwarm sw, const double 
         gmin_lower(sw, 0, i, c);
     }
 #pragma unroll
-    for (int k = 0; k < 3; ++k) push_inbox(sw, 0, i, l + 64 * k, lr[k], ls[k], 1, c, f.th);
+    for (int k = 0; k < 3; ++k) push_inbox(sw, 0, i, l + 64 * k, lk[k], 1, c, f.th);
 }
 
 __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *__restrict__ og,
@@ -449,35 +478,36 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
     const int i = blockIdx.x * PW_WPB + w, P = sw.P, K = sw.K;
     const bool valid = i < P;
     const int ic = valid ? i : P - 1;
-    stage_hand<PW_NT>(hs, Hg);
+    const double hw = hand_word<PW_NT>(Hg);  // staged into LDS before the block barrier
     const DevHand *__restrict__ H = &hs;
     FkSm &f = fks[w];
-    // ---- round 1: every load of the generation, all independent
-    int lr[3], ls[3];
-    push_lane_links(sw, g, ic, l, g + 1, -1, lr, ls);  // var-0 links after the decision
-    const CloudView cv = obs_cloud(o);
+    // ---- round 1: every load of the generation, all independent and unconditional
+    Link lk[3];
+    push_lane_links(sw, g, ic, l, g + 1, -1, lk);  // var-0 links after the decision
+    const CloudGlobal cv = obs_cloud(o);
     const Pt pre = load_pt(cv, l);
     const size_t e = (size_t)ic * HPE_DOF + l;
-    double xo = 0, vo = 0, pbi = 0, rp = 0, rg = 0;
-    if (l < HPE_DOF) {
-        xo = sw.xh[(size_t)(g - 1) * P * HPE_DOF + e];
-        vo = sw.v[e];
-        pbi = sw.pb[e];
-        rp = philox_u01(sw.seed, ST_RP, g, ic, l);
-        rg = philox_u01(sw.seed, ST_RG, g, ic, l);
-    }
+    const size_t ec = (size_t)ic * HPE_DOF + (l < HPE_DOF ? l : HPE_DOF - 1);
+    const double xo = sw.xh[(size_t)(g - 1) * P * HPE_DOF + ec];
+    const double vo = sw.v[ec];
+    const double pbi = sw.pb[ec];
+    const double lbt = sw.bounds[ec - (size_t)ic * HPE_DOF];
+    const double ubt = sw.bounds[ec - (size_t)ic * HPE_DOF + HPE_DOF];
     const double pci = sw.pch[(size_t)(g - 1) * P + ic];
-    const double fmin = gmin_read(sw, g - 1);
-    const Sig pv = sw.sig[g > 1 ? g - 1 : 0];
-    double tg[2] = {0, 0}, tc[2] = {0, 0};
-    if (l < K) {
+    double tg[2], tc[2];
 #pragma unroll
-        for (int vr = 0; vr < 2; ++vr) {
-            const double *sl = sw.inbox + ib_index(sw, (g - 1) & 1, vr, ic, l);
-            tg[vr] = sl[0];
-            tc[vr] = sl[1];
-        }
+    for (int vr = 0; vr < 2; ++vr) {
+        const double *sl = sw.inbox + ib_index(sw, (g - 1) & 1, vr, ic, l < K ? l : K - 1);
+        tg[vr] = sl[0];
+        tc[vr] = sl[1];
     }
+    const unsigned long long gcell = gmin_load(sw, g - 1);
+    const Sig pv = sw.sig[g > 1 ? g - 1 : 0];
+    // the draws while the loads are in flight
+    const int dl = l < HPE_DOF ? l : 0;
+    const double rp = philox_u01(sw.seed, ST_RP, g, ic, dl);
+    const double rg = philox_u01(sw.seed, ST_RG, g, ic, dl);
+    const double fmin = gmin_reduce(gcell);
     // ---- end-of-generation update of g-1 (PSO.cpp:864-877), uniform
     Sig sg;
     if (g == 1) {
@@ -496,7 +526,7 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const int q = l + 64 * k;
-        if (q >= 3 * IB_FIELDS) load_link(sw, g, ic, q, topo, lr[k], ls[k]);
+        if (q >= 3 * IB_FIELDS) lk[k] = load_link(sw, g, ic, q, topo);
     }
     // ---- informant (PSO.cpp:810-812)
     double v = __builtin_inf();
@@ -517,7 +547,6 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
     wave_argmin_lex(v, idx, slot, inf, islot);
     // ---- velocity, position, check_constraints (PSO.cpp:824-842, 358-377)
     if (l < HPE_DOF) {
-        const double *lb = sw.bounds, *ub = sw.bounds + HPE_DOF;
         double vn;
         if (inf == ic) {
             vn = W1 * vo + (C1 * rp) * (pbi - xo);
@@ -527,14 +556,15 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
         }
         double xn = xo + vn;
         const double xr = xn;
-        if (xr < lb[l]) { xn = lb[l]; vn = 0.; }
-        if (xr > ub[l]) { xn = lb[l]; vn = 0.; }  // above max -> MIN (PSO.cpp:372)
+        if (xr < lbt) { xn = lbt; vn = 0.; }
+        if (xr > ubt) { xn = lbt; vn = 0.; }  // above max -> MIN (PSO.cpp:372)
         if (valid) {
             sw.v[e] = vn;
             sw.xh[(size_t)g * P * HPE_DOF + e] = xn;
         }
         f.th[l] = xn;
     }
+    hand_put<PW_NT>(hs, hw);
     __syncthreads();  // hand staged (the only block-wide sync)
     // ---- evaluation and pbest (PSO.cpp:848-861)
     const double fx = eval_wave_cost(f, o, cv, H, pre);
@@ -554,7 +584,7 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const int q = l + 64 * k;
-        push_inbox(sw, g, i, q, lr[k], ls[k], q < 3 * IB_FIELDS ? g + 1 : topo, pn, f.th);
+        push_inbox(sw, g, i, q, lk[k], q < 3 * IB_FIELDS ? g + 1 : topo, pn, f.th);
     }
 }
 
@@ -653,7 +683,7 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
         if (same_eval && last >= 0) return;  // out[26] = gcost = cal_cost(bestp)
         const DevObs o = *og;
         if (t < HPE_DOF) sm.fk.th[t] = out[t];
-        const CloudView cv = obs_cloud(o);
+        const CloudGlobal cv = obs_cloud(o);
         const Pt pre = load_pt(cv, t);
         __syncthreads();
         const double c = eval_block<EV_COST, HPE_NT>(sm, o, cv, &sm.hand, nullptr, pre);
@@ -774,8 +804,8 @@ __device__ __forceinline__ double mw_sum(const MwLeader &ml, int w) {
 
 // rs.f[w] = cal_cost2(rs.w[w].th, matchId, false) for w < nn; each wave has written its
 // own rs.w[w].th.  Ends with a workgroup barrier.
-template <bool MW>
-__device__ __forceinline__ void eval_nodes(RefineSm &rs, int nn, const DevObs &o, const CloudView &cv,
+template <bool MW, class CV>
+__device__ __forceinline__ void eval_nodes(RefineSm &rs, int nn, const DevObs &o, const CV &cv,
                                            const DevHand *__restrict__ H,
                                            const int32_t *__restrict__ match, FkX *Xt,
                                            MwLeader *ml, int *flag) {
@@ -808,15 +838,16 @@ __device__ __forceinline__ void eval_nodes(RefineSm &rs, int nn, const DevObs &o
 }
 
 // f_k = cal_cost2(x0, matchId, true) with the spheres of x0 in rs.base.
-template <bool MW>
-__device__ __forceinline__ double eval_corr(RefineSm &rs, const DevObs &o, const CloudView &cv,
+template <bool MW, class CV>
+__device__ __forceinline__ double eval_corr(RefineSm &rs, const DevObs &o, const CV &cv,
                                             const DevHand *__restrict__ H, int32_t *__restrict__ match,
                                             MwLeader *ml, int *flag) {
     const int t = threadIdx.x;
     if (MW) mw_publish(*ml, rs, MW_JOB_CORR, 1);
-    double dep = (t < HPE_NS) ? depth_term(rs.base, t, o, H) : 0.0;
+    const DepthG dg = depth_issue(rs.base, t, o, H);
     double al = MW ? 0.0 : search_align<RF_NT, true>(rs.base, cv, H, match, load_pt(cv, t));
     double co = (t < 144) ? collide_term(rs.base, t, H) : 0.0;
+    double dep = depth_finish(dg, o, t < HPE_NS);
     block_sum3<RF_NT>(rs.red, al, dep, co);  // also publishes matchId to the block
     if (MW) {
         mw_collect(*ml, flag);
@@ -835,12 +866,11 @@ __device__ void mw_helper(const DevMw &mw, int h, const DevObs *__restrict__ og,
     __shared__ int sh[2];
     const DevObs o = *og;
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
-    for (int q = t; q < (int)(sizeof(DevHand) / 8); q += RF_NT)
-        ((double *)&hs)[q] = ((const double *)Hg)[q];
+    stage_hand<RF_NT>(hs, Hg);
     const DevHand *__restrict__ H = &hs;
     const int Q = mw.Q, per = (o.n + Q - 1) / Q;
     const int s0 = min(h * per, o.n), s1 = min(s0 + per, o.n);
-    const CloudView cs{o.cx + s0, o.cy + s0, o.cz + s0, s1 - s0};
+    const CloudGlobal cs{gp(o.cx) + s0, gp(o.cy) + s0, gp(o.cz) + s0, s1 - s0};
     int32_t *ms = match_g + s0;
     __syncthreads();
     for (unsigned k = 1;; ++k) {
@@ -896,8 +926,8 @@ __device__ void mw_helper(const DevMw &mw, int h, const DevObs *__restrict__ og,
 // goldstein" branch) and the walk replays the serial rules.  Returns tk (0 after 30
 // rejected trials); the accepted node's spheres are copied into rs.base and its cost to
 // *f_acc.  evals grows by the serial evaluation count.
-template <bool MW = false>
-__device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const CloudView &cv,
+template <bool MW = false, class CV>
+__device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const CV &cv,
                                             const DevHand *__restrict__ H,
                                             const int32_t *__restrict__ match, double fk,
                                             double gp, int &evals, double *f_acc,
@@ -1010,21 +1040,22 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
     __shared__ RefineSm rs;
     __shared__ DevHand hs;  // hand constants in LDS: keeps them out of the loop's registers
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
-    for (int q = t; q < (int)(sizeof(DevHand) / 8); q += RF_NT)
-        ((double *)&hs)[q] = ((const double *)Hg)[q];
+    stage_hand<RF_NT>(hs, Hg);
     const DevHand *__restrict__ H = &hs;
-    CloudView cv = obs_cloud(o);
+    using CV = std::conditional_t<STAGED, CloudView, CloudGlobal>;
+    CV cv;
     int32_t *match = match_g;
     if (STAGED) {
         double *cx = (double *)dyn, *cy = cx + o.n, *cz = cy + o.n;
         for (int p = t; p < o.n; p += RF_NT) {
-            cx[p] = o.cx[p];
-            cy[p] = o.cy[p];
-            cz[p] = o.cz[p];
+            cx[p] = gp(o.cx)[p];
+            cy[p] = gp(o.cy)[p];
+            cz[p] = gp(o.cz)[p];
         }
-        cv = CloudView{cx, cy, cz, o.n};
+        if constexpr (STAGED) cv = CV{cx, cy, cz, o.n};
         match = (int32_t *)(cz + o.n);
     }
+    if constexpr (!STAGED) cv = obs_cloud(o);
     if (t < HPE_DOF) rs.x0[t] = x0g[t];
     __shared__ int mwflag;
     MwLeader ml{mw, 0u, false};
@@ -1148,6 +1179,17 @@ __global__ void k_render(const double *__restrict__ S, const DevHand *__restrict
 }
 
 #if HPE_STAMPS
+// Diagnostic build only: per-block k_pso_gen stamps, then cleared (not part of include/hpe.h).
+extern "C" int hpe_debug_blk_ts(unsigned long long *out) {
+    if (!out) return HPE_E_ARG;
+    const size_t nb = sizeof(unsigned long long) * BT_GENS * BT_BLK * BT_PTS;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hpe_blk_ts), nb, 0, hipMemcpyDeviceToHost) != hipSuccess)
+        return HPE_E_HIP;
+    std::vector<unsigned long long> z(BT_GENS * BT_BLK * BT_PTS, 0ull);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(hpe_blk_ts), z.data(), nb, 0, hipMemcpyHostToDevice) != hipSuccess)
+        return HPE_E_HIP;
+    return HPE_OK;
+}
 // Diagnostic build only: the Goldstein decision log (not part of include/hpe.h).
 extern "C" int hpe_debug_gold_log(unsigned long long *out, int n) {
     if (!out || n < 1) return HPE_E_ARG;

@@ -71,7 +71,7 @@ __global__ __launch_bounds__(HPE_NT) void k_opt_init(DevOpt op, const double *__
         op.pb[e] = x;
         op.v[e] = 0.0;
     }
-    const CloudView cv = obs_cloud(o);
+    const CloudGlobal cv = obs_cloud(o);
     const Pt pre = load_pt(cv, t);
     __syncthreads();
     const double c = eval_block<EV_COST, HPE_NT>(sm, o, cv, H, nullptr, pre);
@@ -92,21 +92,22 @@ __global__ __launch_bounds__(RF_NT) void k_opt_descent(DevOpt op, const DevObs *
     __shared__ int sel_s[OPT_GRADITER];
     __shared__ int flag;
     const int i = blockIdx.x, t = threadIdx.x, w = t >> 6, l = t & 63;
-    for (int q = t; q < (int)(sizeof(DevHand) / 8); q += RF_NT)
-        ((double *)&hs)[q] = ((const double *)Hg)[q];
+    stage_hand<RF_NT>(hs, Hg);
     const DevHand *__restrict__ H = &hs;
-    CloudView cv = obs_cloud(o);
+    using CV = std::conditional_t<STAGED, CloudView, CloudGlobal>;
+    CV cv;
     int32_t *match = op.match + (size_t)i * op.n_cap;
     if (STAGED) {
         double *cx = (double *)dyn, *cy = cx + o.n, *cz = cy + o.n;
         for (int p = t; p < o.n; p += RF_NT) {
-            cx[p] = o.cx[p];
-            cy[p] = o.cy[p];
-            cz[p] = o.cz[p];
+            cx[p] = gp(o.cx)[p];
+            cy[p] = gp(o.cy)[p];
+            cz[p] = gp(o.cz)[p];
         }
-        cv = CloudView{cx, cy, cz, o.n};
+        if constexpr (STAGED) cv = CV{cx, cy, cz, o.n};
         match = (int32_t *)(cz + o.n);
     }
+    if constexpr (!STAGED) cv = obs_cloud(o);
     const size_t e = (size_t)i * HPE_DOF + t;
     double vel = 0.0;
     if (t < HPE_DOF) {
@@ -132,9 +133,10 @@ __global__ __launch_bounds__(RF_NT) void k_opt_descent(DevOpt op, const DevObs *
             __syncthreads();
             if (w == 0) fk_wave(rs.base, H);
             __syncthreads();
-            double dep = (t < HPE_NS) ? depth_term(rs.base, t, o, H) : 0.0;
+            const DepthG dg = depth_issue(rs.base, t, o, H);
             double al = search_align<RF_NT, true>(rs.base, cv, H, match, load_pt(cv, t));
             double co = (t < 144) ? collide_term(rs.base, t, H) : 0.0;
+            double dep = depth_finish(dg, o, t < HPE_NS);
             block_sum3<RF_NT>(rs.red, al, dep, co);
             fk = (al * o.lambda + dep) + co;
             sc.lap(26);
@@ -169,9 +171,10 @@ __global__ __launch_bounds__(RF_NT) void k_opt_descent(DevOpt op, const DevObs *
         double f2 = fk;  // tk == 0: theta unchanged, same matchId -> same cost
         if (tk != 0) {
             if (m == 0) {  // cal_cost2(ctheta, matchId, true): rs.base holds the new spheres
-                double dep = (t < HPE_NS) ? depth_term(rs.base, t, o, H) : 0.0;
+                const DepthG dg = depth_issue(rs.base, t, o, H);
                 double al = search_align<RF_NT, true>(rs.base, cv, H, match, load_pt(cv, t));
                 double co = (t < 144) ? collide_term(rs.base, t, H) : 0.0;
+                double dep = depth_finish(dg, o, t < HPE_NS);
                 block_sum3<RF_NT>(rs.red, al, dep, co);
                 f2 = (al * o.lambda + dep) + co;
             } else {
@@ -228,7 +231,7 @@ __global__ __launch_bounds__(HPE_NT) void k_opt_move(DevOpt op, const DevObs *__
         op.x[e] = xn;
         sm.fk.th[t] = xn;
     }
-    const CloudView cv = obs_cloud(o);
+    const CloudGlobal cv = obs_cloud(o);
     const Pt pre = load_pt(cv, t);
     __syncthreads();
     const double fx = eval_block<EV_COST, HPE_NT>(sm, o, cv, H, nullptr, pre);

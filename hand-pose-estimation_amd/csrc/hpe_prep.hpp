@@ -283,22 +283,41 @@ __device__ __forceinline__ void prep_dt(const PrepArgs &a, unsigned char *lds) {
     unsigned *msk = (unsigned *)(lds + PREP_CH * 8 + 64 + 2 * (PREP_NT / 64) * 4);
     float *wmaxp = (float *)(msk + W * H / 32);
     const int t = threadIdx.x, l = t & 63;
-    for (int p0 = 0; p0 < W * H; p0 += 4 * PREP_NT) {  // hand = non-zero raw depth
-        float v[4];
+    // hand = non-zero raw depth: 150 pixels per thread, loads issued 30 at a time
+    // (unconditional: no branch splits them into one round trip each)
+    constexpr int NPT = W * H / PREP_NT, B = 30;
+    static_assert(W * H % PREP_NT == 0 && NPT % B == 0, "whole batches");
+    for (int k0 = 0; k0 < NPT; k0 += B) {
+        float v[B];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int pix = p0 + q * PREP_NT + t;
-            v[q] = (pix < W * H) ? a.raw[pix] : 0.f;
-        }
+        for (int q = 0; q < B; ++q) v[q] = a.raw[(k0 + q) * PREP_NT + t];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < B; ++q) {
             const unsigned long long bm = __ballot(v[q] != 0.f);
-            const int pix = p0 + q * PREP_NT + t;
-            if ((l & 31) == 0 && pix < W * H) msk[pix >> 5] = (unsigned)(bm >> (l & 32));
+            const int pix = (k0 + q) * PREP_NT + t;
+            if ((l & 31) == 0) msk[pix >> 5] = (unsigned)(bm >> (l & 32));
         }
     }
-    if (t == 0) msk[W * H / 32] = 0u;  // the two-word window of the last pixels
+    int *rfirst = (int *)(msk + W * H / 32 + 1);
+    if (t == 0) {
+        msk[W * H / 32] = 0u;  // the two-word window of the last pixels
+        *rfirst = 0x7FFFFFFF;
+    }
     __syncthreads();
+    for (int k = t; k < W * H / 32; k += PREP_NT) {  // first mask word holding a hand pixel
+        if (msk[k] != 0u) {
+            atomicMin(rfirst, k);
+            break;
+        }
+    }
+    __syncthreads();
+    // The forward pass starts at the first row r0 holding a hand pixel.  Above it every
+    // forward value is >= DT_INIT; with a hand pixel anywhere, every pixel's final value is
+    // finite (< DT_INIT: a forward path right/down from some hand pixel, then a backward
+    // path up/left, stays inside the image), so forward values >= DT_INIT never win a min
+    // and any such value gives the same result: the rows above r0 start from DT_INIT, as
+    // row 0 does, and the backward pass reads DT_INIT for them.  No hand pixel: r0 = 0.
+    const int r0 = (*rfirst == 0x7FFFFFFF) ? 0 : *rfirst / (W / 32);
     if (t < 64) {
         // forward pass: lane l owns columns c0..c0+4; u1 / u2 = rows r-1 / r-2 at columns
         // c0-2 .. c0+6 (halo from the neighbour lanes)
@@ -307,7 +326,7 @@ __device__ __forceinline__ void prep_dt(const PrepArgs &a, unsigned char *lds) {
 #pragma unroll
         for (int i = 0; i < 9; ++i) u1[i] = u2[i] = DT_INIT;
 #pragma unroll 2
-        for (int r = 0; r < H; ++r) {
+        for (int r = r0; r < H; ++r) {
             const int pix0 = r * W + c0;
             const unsigned long long mw =
                 ((unsigned long long)msk[(pix0 >> 5) + 1] << 32) | msk[pix0 >> 5];
@@ -352,13 +371,24 @@ __device__ __forceinline__ void prep_dt(const PrepArgs &a, unsigned char *lds) {
         for (int i = 0; i < 9; ++i) d1[i] = d2[i] = DT_INIT;
         float mx = 0.f;
         const float sc = 1.f / 65536;
-        int fw[5], fn[5];
+        // forward values three rows ahead: row r's values are loaded while row r+3 is
+        // scanned, into the register slot row r+3 just consumed (three slots, the loop
+        // unrolled by three, so no register copy makes a row wait for newer loads);
+        // unconditional loads of a clamped row
+        int f0[5], f1[5], f2[5];
 #pragma unroll
-        for (int k = 0; k < 5; ++k) fw[k] = a.dtf[(H - 1) * W + cb - k];
-#pragma unroll 2
-        for (int r = H - 1; r >= 0; --r) {
+        for (int k = 0; k < 5; ++k) {
+            f0[k] = a.dtf[(H - 1) * W + cb - k];
+            f1[k] = a.dtf[(H - 2) * W + cb - k];
+            f2[k] = a.dtf[(H - 3) * W + cb - k];
+        }
+        auto step = [&](int r, int (&fs)[5]) {
+            int fw[5];
 #pragma unroll
-            for (int k = 0; k < 5; ++k) fn[k] = (r > 0) ? a.dtf[(r - 1) * W + cb - k] : 0;
+            for (int k = 0; k < 5; ++k) fw[k] = (r >= r0) ? fs[k] : DT_INIT;  // rows above r0: not scanned
+            const int rn = r >= 3 ? r - 3 : 0;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) fs[k] = a.dtf[rn * W + cb - k];
             int q[5], p[5];
 #pragma unroll
             for (int k = 0; k < 5; ++k) {
@@ -387,8 +417,12 @@ __device__ __forceinline__ void prep_dt(const PrepArgs &a, unsigned char *lds) {
             for (int k = 0; k < 5; ++k) d1[k + 2] = T[k];
             d1[7] = from_right(T[0], DT_INIT);
             d1[8] = from_right(T[1], DT_INIT);
-#pragma unroll
-            for (int k = 0; k < 5; ++k) fw[k] = fn[k];
+        };
+        static_assert(H % 3 == 0, "backward rows in threes");
+        for (int r = H - 1; r >= 2; r -= 3) {
+            step(r, f0);
+            step(r - 1, f1);
+            step(r - 2, f2);
         }
         for (int off = 32; off > 0; off >>= 1) {
             const float o = __shfl_xor(mx, off);
