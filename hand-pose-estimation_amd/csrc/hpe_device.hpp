@@ -35,7 +35,7 @@ __device__ unsigned long long hpe_gold_log[1 + HPE_GOLD_LOG];  // [0] = count
 // [generation][block][point], written by thread 0 (diagnostic build only).
 #define BT_GENS 48
 #define BT_BLK 256
-#define BT_PTS 8
+#define BT_PTS 24
 #if HPE_STAMPS
 __device__ unsigned long long hpe_blk_ts[BT_GENS * BT_BLK * BT_PTS];
 #define BLK_TS(g, k)                                                                       \
@@ -43,7 +43,17 @@ __device__ unsigned long long hpe_blk_ts[BT_GENS * BT_BLK * BT_PTS];
         if (threadIdx.x == 0 && (g) < BT_GENS && blockIdx.x < BT_BLK)                      \
             hpe_blk_ts[((g) * BT_BLK + blockIdx.x) * BT_PTS + (k)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
+// the same from lane 0 of every wave (point k + wave)
+#define WAVE_TS(g, k)                                                                      \
+    do {                                                                                   \
+        if ((threadIdx.x & 63) == 0 && (g) < BT_GENS && blockIdx.x < BT_BLK)               \
+            hpe_blk_ts[((g) * BT_BLK + blockIdx.x) * BT_PTS + (k) + (threadIdx.x >> 6)] =  \
+                __builtin_amdgcn_s_memrealtime();                                          \
+    } while (0)
 #else
+#define WAVE_TS(g, k) \
+    do {              \
+    } while (0)
 #define BLK_TS(g, k) \
     do {             \
     } while (0)
@@ -348,6 +358,27 @@ __device__ __forceinline__ void wave_argmin_lex(double v, int idx, int pay, int 
     out_pay = __builtin_amdgcn_readlane(pay, (int)__ffsll((long long)b) - 1);
 }
 
+// The same over lanes 0..15 only (row 0; the other lanes are ignored): four DPP steps per
+// key inside the row and one readlane each, instead of the cross-row readlane chains.
+__device__ __forceinline__ void row0_argmin_lex(double v, int idx, int pay, int &out_idx,
+                                                int &out_pay) {
+    double m = v;
+    m = fmin(m, dpp_f64<0xB1>(m));
+    m = fmin(m, dpp_f64<0x4E>(m));
+    m = fmin(m, dpp_f64<0x141>(m));
+    m = fmin(m, dpp_f64<0x140>(m));
+    const double mn = readlane_f64(m, 0);
+    int c = (v == mn) ? idx : 0x7fffffff;
+    c = min(c, dpp_i32<0xB1>(c));
+    c = min(c, dpp_i32<0x4E>(c));
+    c = min(c, dpp_i32<0x141>(c));
+    c = min(c, dpp_i32<0x140>(c));
+    const int mi = __builtin_amdgcn_readlane(c, 0);
+    const unsigned long long b = __ballot(v == mn && idx == mi) & 0xffffull;
+    out_idx = mi;
+    out_pay = __builtin_amdgcn_readlane(pay, (int)__ffsll((long long)b) - 1);
+}
+
 // three independent sums interleaved for ILP
 __device__ __forceinline__ void wave_sum3(double &a, double &b, double &c) {
     a += dpp_f64<0xB1>(a); b += dpp_f64<0xB1>(b); c += dpp_f64<0xB1>(c);
@@ -434,6 +465,14 @@ __device__ __forceinline__ double depth_finish(DepthG d, const DevObs &o, bool u
     const double v = !d.in ? md * md : (d.djc != 0.0) ? diff * diff : dd * dd;
     return use ? v : 0.0;
 }
+// Block form: wave 0 (its lanes 0..47 are the spheres) issues; the other waves keep a
+// zero DepthG, so they spend no VALU time on the projections while they search.
+__device__ __forceinline__ DepthG depth_issue_w0(const FkSm &f, const DevObs &o,
+                                                 const DevHand *__restrict__ H) {
+    DepthG d{0.0, 0.0, 0.0, 0.f, false};
+    if (threadIdx.x < 64) d = depth_issue(f, threadIdx.x, o, H);
+    return d;
+}
 __device__ __forceinline__ double depth_term(const FkSm &f, int i, const DevObs &o,
                                              const DevHand *__restrict__ H) {
     return depth_finish(depth_issue(f, i, o, H), o, true);
@@ -494,12 +533,13 @@ template <int NT, bool STORE_MATCH, class CV>
 __device__ __forceinline__ double search_align(const FkSm &f, const CV &cv,
                                                const DevHand *__restrict__ H,
                                                int32_t *__restrict__ match, Pt pre,
-                                               int gt = -1) {
+                                               int gt = -1, int g_ts = BT_GENS) {
     if (gt < 0) gt = threadIdx.x;
     double acc = 0.0;
     const int h = gt & 1;
     typedef float f2 __attribute__((ext_vector_type(2)));  // packed fp32 (v_pk_*_f32)
     const float *SX = f.Sp[0] + 24 * h, *SY = f.Sp[1] + 24 * h, *SZ = f.Sp[2] + 24 * h;
+    BLK_TS(g_ts, 15);
     for (int it = gt; it < 2 * cv.n; it += NT) {
         const int p = it >> 1;
         const Pt q = (it == gt) ? pre : load_pt(cv, it);
@@ -518,9 +558,12 @@ __device__ __forceinline__ double search_align(const FkSm &f, const CV &cv,
             d2[j + 1] = d.y;
             m = fminf(m, fminf(d.x, d.y));
         }
+        BLK_TS(g_ts, 11);
         m = fminf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0xB1, 0xf, 0xf,
                                                                false)));  // partner lane t^1
         const float hi = hi_sqrt_class(m);
+        if (HPE_STAMPS) asm volatile("" ::"v"(hi));
+        BLK_TS(g_ts, 12);
         // first j with d2[j] <= hi, branch-free: key_j = j, or j + 64 when d2[j] > hi
         // (non-negative floats order like their bit patterns), then an integer min tree
         const int hb = __float_as_int(hi);
@@ -537,6 +580,8 @@ __device__ __forceinline__ double search_align(const FkSm &f, const CV &cv,
                       min(min(key[12], key[15]), min(key[18], key[21])));
         idx = (idx >= 64) ? (1 << 20) : idx + 24 * h;
         idx = min(idx, __builtin_amdgcn_mov_dpp(idx, 0xB1, 0xf, 0xf, false));
+        if (HPE_STAMPS) asm volatile("" ::"v"(idx));
+        BLK_TS(g_ts, 13);
         if (h == 0) {
             if (idx >= HPE_NS) idx = 0;  // all-NaN point: reference is undefined (trainIdx -1)
             const double dx = X - f.S[idx][0], dy = Y - f.S[idx][1], dz = Z - f.S[idx][2];
@@ -544,6 +589,8 @@ __device__ __forceinline__ double search_align(const FkSm &f, const CV &cv,
             acc += e * e;
             if (STORE_MATCH) match[p] = idx;
         }
+        if (HPE_STAMPS) asm volatile("" ::"v"(acc));
+        BLK_TS(g_ts, 14);
     }
     return acc;
 }
@@ -611,7 +658,8 @@ __device__ __forceinline__ CloudGlobal obs_cloud(const DevObs &o) {
 template <int MODE, int NT, bool FK = true, class CV>
 __device__ __forceinline__ double eval_block(Smem &sm, const DevObs &o, const CV &cv,
                                              const DevHand *__restrict__ H,
-                                             int32_t *__restrict__ match, Pt pre) {
+                                             int32_t *__restrict__ match, Pt pre,
+                                             int g_ts = BT_GENS) {
     StampClock sc;
     sc.start();
     if (FK) {
@@ -621,15 +669,19 @@ __device__ __forceinline__ double eval_block(Smem &sm, const DevObs &o, const CV
     sc.lap(10);
     const int t = threadIdx.x;
     // issue the depth gathers first: their latency hides under the search
-    const DepthG dg = depth_issue(sm.fk, t, o, H);
+    const DepthG dg = depth_issue_w0(sm.fk, o, H);
     double al;
     if (MODE == EV_COST2_FROZEN) al = align_frozen(sm.fk, cv, H, match, t, NT);
     else if (MODE == EV_COST2_CORR || MODE == EV_COST_STORE)
         al = search_align<NT, true>(sm.fk, cv, H, match, pre);
-    else al = search_align<NT, false>(sm.fk, cv, H, nullptr, pre);
+    else al = search_align<NT, false>(sm.fk, cv, H, nullptr, pre, -1, g_ts);
     const bool coll = (MODE == EV_COST2_CORR || MODE == EV_COST2_FROZEN);
     double co = (coll && t < 144) ? collide_term(sm.fk, t, H) : 0.0;
+    BLK_TS(g_ts, 8);
     double dep = depth_finish(dg, o, t < HPE_NS);
+    BLK_TS(g_ts, 9);
+    if (HPE_STAMPS) asm volatile("" ::"v"(al), "v"(dep));
+    WAVE_TS(g_ts, 16);
     sc.lap(11);
     block_sum3<NT, false, !(MODE == EV_COST2_CORR || MODE == EV_COST2_FROZEN)>(sm.red, al, dep, co);
     sc.lap(12);

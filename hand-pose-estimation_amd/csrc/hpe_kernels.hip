@@ -314,6 +314,7 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
         const unsigned long long gcell = gmin_load(sw, g - 1);
         const Sig pv = sw.sig[g > 1 ? g - 1 : 0];
         const double fmin = gmin_reduce(gcell);  // NaN when no value was written
+        BLK_TS(g, 6);
         // end-of-generation update of g-1 (PSO.cpp:864-877) / initial gbest (:755-760),
         // computed redundantly by every lane (uniform values)
         Sig sg;
@@ -337,6 +338,8 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
         var = (topo == g) ? 1 : 0;
         sc.lap(0);
         // informant = first argmin of pbest cost over {i} U incoming (PSO.cpp:810-812)
+        // candidates in lanes 0..K-1, self in lane 15 (K <= 15: one 16-lane row) or 63
+        const int self_lane = (K <= 15) ? 15 : 63;
         double v = __builtin_inf();
         int idx = 0x7fffffff, slot = -1;
         if (t < K) {
@@ -346,12 +349,14 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
                 idx = (int)(tag & 0xffffffff);
                 slot = t;
             }
-        } else if (t == 63) {  // self (L = eye)
+        } else if (t == self_lane) {  // self (L = eye)
             v = pci;
             idx = i;
         }
         if (v != v) v = __builtin_inf();
-        wave_argmin_lex(v, idx, slot, inf, islot);
+        if (K <= 15) row0_argmin_lex(v, idx, slot, inf, islot);
+        else wave_argmin_lex(v, idx, slot, inf, islot);
+        BLK_TS(g, 7);
         sc.lap(1);
     }
     hand_put<HPE_NT>(sm.hand, hw);
@@ -379,6 +384,7 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
             sm.fk.th[t] = xn;
         }
         wave_sync();
+        BLK_TS(g, 10);
         sc.lap(2);
         fk_wave(sm.fk, H);
     }
@@ -388,7 +394,7 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
     const double pci = sm.dscal[4];
     const Link lk0 = load_link(sw, g, i, q, topo, q >= 3 * IB_FIELDS);
     // ---- evaluation and pbest (PSO.cpp:848-861)
-    const double fx = eval_block<EV_COST, HPE_NT, false>(sm, o, cv, H, nullptr, pre);
+    const double fx = eval_block<EV_COST, HPE_NT, false>(sm, o, cv, H, nullptr, pre, g);
     BLK_TS(g, 4);
     sc.start();
     const bool better = fx < pci;
@@ -529,6 +535,7 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
         if (q >= 3 * IB_FIELDS) lk[k] = load_link(sw, g, ic, q, topo);
     }
     // ---- informant (PSO.cpp:810-812)
+    const int self_lane = (K <= 15) ? 15 : 63;  // one 16-lane row when K <= 15
     double v = __builtin_inf();
     int idx = 0x7fffffff, slot = -1;
     if (l < K) {
@@ -538,13 +545,14 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
             idx = (int)(tag & 0xffffffff);
             slot = l;
         }
-    } else if (l == 63) {
+    } else if (l == self_lane) {
         v = pci;
         idx = ic;
     }
     if (v != v) v = __builtin_inf();
     int inf, islot;
-    wave_argmin_lex(v, idx, slot, inf, islot);
+    if (K <= 15) row0_argmin_lex(v, idx, slot, inf, islot);
+    else wave_argmin_lex(v, idx, slot, inf, islot);
     // ---- velocity, position, check_constraints (PSO.cpp:824-842, 358-377)
     if (l < HPE_DOF) {
         double vn;
@@ -844,7 +852,7 @@ __device__ __forceinline__ double eval_corr(RefineSm &rs, const DevObs &o, const
                                             MwLeader *ml, int *flag) {
     const int t = threadIdx.x;
     if (MW) mw_publish(*ml, rs, MW_JOB_CORR, 1);
-    const DepthG dg = depth_issue(rs.base, t, o, H);
+    const DepthG dg = depth_issue_w0(rs.base, o, H);
     double al = MW ? 0.0 : search_align<RF_NT, true>(rs.base, cv, H, match, load_pt(cv, t));
     double co = (t < 144) ? collide_term(rs.base, t, H) : 0.0;
     double dep = depth_finish(dg, o, t < HPE_NS);

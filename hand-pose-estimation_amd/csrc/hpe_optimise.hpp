@@ -133,7 +133,7 @@ __global__ __launch_bounds__(RF_NT) void k_opt_descent(DevOpt op, const DevObs *
             __syncthreads();
             if (w == 0) fk_wave(rs.base, H);
             __syncthreads();
-            const DepthG dg = depth_issue(rs.base, t, o, H);
+            const DepthG dg = depth_issue_w0(rs.base, o, H);
             double al = search_align<RF_NT, true>(rs.base, cv, H, match, load_pt(cv, t));
             double co = (t < 144) ? collide_term(rs.base, t, H) : 0.0;
             double dep = depth_finish(dg, o, t < HPE_NS);
@@ -171,7 +171,7 @@ __global__ __launch_bounds__(RF_NT) void k_opt_descent(DevOpt op, const DevObs *
         double f2 = fk;  // tk == 0: theta unchanged, same matchId -> same cost
         if (tk != 0) {
             if (m == 0) {  // cal_cost2(ctheta, matchId, true): rs.base holds the new spheres
-                const DepthG dg = depth_issue(rs.base, t, o, H);
+                const DepthG dg = depth_issue_w0(rs.base, o, H);
                 double al = search_align<RF_NT, true>(rs.base, cv, H, match, load_pt(cv, t));
                 double co = (t < 144) ? collide_term(rs.base, t, H) : 0.0;
                 double dep = depth_finish(dg, o, t < HPE_NS);

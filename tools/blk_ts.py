@@ -20,7 +20,7 @@ lib.hpe_debug_blk_ts.restype = C.c_int
 lib.hpe_debug_blk_ts.argtypes = [C.POINTER(C.c_uint64)]
 nfr = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 P = int(sys.argv[2]) if len(sys.argv) > 2 else 256
-GENS, BLK, PTS = 48, 256, 8
+GENS, BLK, PTS = 48, 256, 24
 hand = hpe.reference_hand()
 ctx = hand.ctx
 poses = synth.trajectory(nfr + 1, 0)
@@ -56,6 +56,15 @@ for g in range(1, 31):
     rows.append((g, (t1 - t0) / 100, ramp, gap, *med, *mx))
     print(f"{g:3d} {(t1 - t0) / 100:8.2f} {ramp:8.2f} {gap:8.2f} | " +
           " ".join(f"{v:6.2f}" for v in med) + " | " + " ".join(f"{v:6.2f}" for v in mx))
+    if g == 1 or g == 15:
+        # finer points (median over blocks, us from entry): 6 round-1 loads landed,
+        # 7 informant done, 1 pre-barrier, 2 post-barrier, 10 velocity done, 3 FK done,
+        # 15 search start, 11 distances, 12 sqrt class, 13 index, 14 residual, 8 search done, 9 depth done, 4 eval done, 5 end
+        rel = (t - t[:, :1]) / 100
+        print("     points from entry:", " ".join(f"{k}:{np.median(rel[:, k]):.2f}"
+                                            for k in (6, 7, 1, 2, 10, 3, 15, 11, 12, 13, 14, 8, 9, 4, 5)))
+        print("     waves at the reduction:", " ".join(f"w{k - 16}:{np.median(rel[:, k]):.2f}"
+                                                 for k in range(16, 24)))
 r = np.array(rows)
 print("mean span %.2f  ramp %.2f  gap %.2f | median phases %s" %
       (r[:, 1].mean(), r[:, 2].mean(), np.nanmean(r[:, 3]),
