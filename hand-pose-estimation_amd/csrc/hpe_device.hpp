@@ -561,25 +561,40 @@ __device__ __forceinline__ double search_align(const FkSm &f, const CV &cv,
         BLK_TS(g_ts, 11);
         m = fminf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0xB1, 0xf, 0xf,
                                                                false)));  // partner lane t^1
-        const float hi = hi_sqrt_class(m);
-        if (HPE_STAMPS) asm volatile("" ::"v"(hi));
-        BLK_TS(g_ts, 12);
-        // first j with d2[j] <= hi, branch-free: key_j = j, or j + 64 when d2[j] > hi
-        // (non-negative floats order like their bit patterns), then an integer min tree
-        const int hb = __float_as_int(hi);
-        int key[24];
+        // first j with bits(d2[j]) <= hb, branch-free: key_j = j, or j + 64 when
+        // d2[j] > hb (non-negative floats order like their bit patterns), then an
+        // integer min tree and the partner lane's half
+        auto first_le = [&](int hb) {
+            int key[24];
 #define HPE_KEY(J) key[J] = sqrt_class_key<J>(hb, d2[J]);
-        HPE_KEY(0) HPE_KEY(1) HPE_KEY(2) HPE_KEY(3) HPE_KEY(4) HPE_KEY(5) HPE_KEY(6) HPE_KEY(7)
-        HPE_KEY(8) HPE_KEY(9) HPE_KEY(10) HPE_KEY(11) HPE_KEY(12) HPE_KEY(13) HPE_KEY(14)
-        HPE_KEY(15) HPE_KEY(16) HPE_KEY(17) HPE_KEY(18) HPE_KEY(19) HPE_KEY(20) HPE_KEY(21)
-        HPE_KEY(22) HPE_KEY(23)
+            HPE_KEY(0) HPE_KEY(1) HPE_KEY(2) HPE_KEY(3) HPE_KEY(4) HPE_KEY(5) HPE_KEY(6) HPE_KEY(7)
+            HPE_KEY(8) HPE_KEY(9) HPE_KEY(10) HPE_KEY(11) HPE_KEY(12) HPE_KEY(13) HPE_KEY(14)
+            HPE_KEY(15) HPE_KEY(16) HPE_KEY(17) HPE_KEY(18) HPE_KEY(19) HPE_KEY(20) HPE_KEY(21)
+            HPE_KEY(22) HPE_KEY(23)
 #undef HPE_KEY
 #pragma unroll
-        for (int j = 0; j < 24; j += 3) key[j] = min(min(key[j], key[j + 1]), key[j + 2]);
-        int idx = min(min(min(key[0], key[3]), min(key[6], key[9])),
-                      min(min(key[12], key[15]), min(key[18], key[21])));
-        idx = (idx >= 64) ? (1 << 20) : idx + 24 * h;
-        idx = min(idx, __builtin_amdgcn_mov_dpp(idx, 0xB1, 0xf, 0xf, false));
+            for (int j = 0; j < 24; j += 3) key[j] = min(min(key[j], key[j + 1]), key[j + 2]);
+            int ix = min(min(min(key[0], key[3]), min(key[6], key[9])),
+                         min(min(key[12], key[15]), min(key[18], key[21])));
+            ix = (ix >= 64) ? (1 << 20) : ix + 24 * h;
+            return min(ix, __builtin_amdgcn_mov_dpp(ix, 0xB1, 0xf, 0xf, false));
+        };
+        // BFMatcher's match is the first j with d2[j] <= hi = hi_sqrt_class(m) (the sqrt
+        // class of the minimum), and hi lies within 4 ulps above m (the class of s =
+        // sqrtf(m) is narrower than 2 s ulp(s) <= 4 ulp(m)).  So the first j within 5 ulps
+        // is the match whenever its own d2 IS the minimum; only otherwise (a sphere within
+        // 5 ulps of the nearest, ahead of it: rare) is the exact class needed, by the whole
+        // wave.  The check recomputes that sphere's fp32 d2 with the search's operations.
+        int idx = first_le(__float_as_int(m) + 5);
+        bool exact = true;
+        if (h == 0) {
+            const int ic = idx < HPE_NS ? idx : 0;
+            const float tx = qx - (float)f.S[ic][0], ty = qy - (float)f.S[ic][1],
+                        tz = qz - (float)f.S[ic][2];
+            const float dc = (tx * tx + ty * ty) + tz * tz;
+            exact = (dc == m);  // false for NaN
+        }
+        if (__ballot(!exact)) idx = first_le(__float_as_int(hi_sqrt_class(m)));
         if (HPE_STAMPS) asm volatile("" ::"v"(idx));
         BLK_TS(g_ts, 13);
         if (h == 0) {

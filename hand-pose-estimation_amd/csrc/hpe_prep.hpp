@@ -325,8 +325,10 @@ __device__ __forceinline__ void prep_dt(const PrepArgs &a, unsigned char *lds) {
         int u1[9], u2[9];
 #pragma unroll
         for (int i = 0; i < 9; ++i) u1[i] = u2[i] = DT_INIT;
-#pragma unroll 2
-        for (int r = r0; r < H; ++r) {
+        // rows in pairs from the even row at or above r0 (a row above r0 scanned from
+        // DT_INIT is as good as unscanned, see above), two rows per trip
+        static_assert(H % 2 == 0, "forward rows in pairs");
+        auto row = [&](int r) {
             const int pix0 = r * W + c0;
             const unsigned long long mw =
                 ((unsigned long long)msk[(pix0 >> 5) + 1] << 32) | msk[pix0 >> 5];
@@ -360,6 +362,10 @@ __device__ __forceinline__ void prep_dt(const PrepArgs &a, unsigned char *lds) {
             for (int k = 0; k < 5; ++k) u1[k + 2] = T[k];
             u1[7] = from_right(T[0], DT_INIT);
             u1[8] = from_right(T[1], DT_INIT);
+        };
+        for (int r = r0 & ~1; r < H; r += 2) {
+            row(r);
+            row(r + 1);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
