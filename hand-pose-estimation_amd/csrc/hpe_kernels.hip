@@ -612,12 +612,22 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
                                                       const DevObs *__restrict__ og = nullptr,
                                                       const DevHand *__restrict__ Hg = nullptr,
                                                       DevObs *__restrict__ obs_out = nullptr,
-                                                      int same_eval = 0) {
+                                                      int same_eval = 0,
+                                                      unsigned long long *__restrict__ seq_dev = nullptr,
+                                                      unsigned long long *done_host = nullptr) {
     constexpr int CH = 2048;  // generations staged per pass
     __shared__ Smem sm;
     __shared__ double gm[CH];
     __shared__ int tp[CH];
     const int t = threadIdx.x, G = sw.G, P = sw.P;
+    if (TAIL && seq_dev && t == 0) {
+        // pipelined tracking: this frame's refine launch (and the preparation of the next
+        // frame inside it, which read a pinned host buffer) has completed; publish the
+        // frame's sequence number to the host, which polls it before reusing that buffer
+        const unsigned long long n = *seq_dev + 1;
+        *seq_dev = n;
+        __hip_atomic_store(done_host, n, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     if (TAIL) stage_hand<HPE_NT>(sm.hand, Hg);
     double gcost = 1e100;
     int last = -1, count = 100;

@@ -48,7 +48,7 @@ struct PrepArgs {
     int *dtf;
     PrepInfo *info;
     DevObs *obs_out;
-    unsigned *ctr;  // [0] bands arrived, [1] (merged cloud, DT) arrived
+    unsigned *ctr;  // [0] bands arrived, [1] (merged cloud, DT) arrived, [2] DT has its mask
 };
 
 // LDS layout: chunk[PREP_CH] doubles | acc1, flag (64 B) | wcnt, hcnt | mask bits | wmax
@@ -147,12 +147,24 @@ __device__ __forceinline__ void prep_band(const PrepArgs &a, int b, unsigned cha
     const int pbase = b * PREP_BAND_PIX;
     double *tmpb = a.tmp + 3 * (size_t)pbase, *ctbb = a.ctb + pbase;
     int base = 0, ncm = 0;
-    float rnext = a.raw[pbase + t];  // one pass ahead: the load latency hides under the pass
-    for (int p0 = 0; p0 < PREP_BAND_PIX; p0 += PREP_NT) {
+    if (t == 0) {  // after the DT workgroup's raw reads (bounded: ~1 ms, then go anyway)
+        for (int i = 0; i < 4096 && __hip_atomic_load(&a.ctr[2], __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT) == 0u; ++i)
+            __builtin_amdgcn_s_sleep(8);
+    }
+    __syncthreads();
+    // the band's raw pixels, all loads in flight at once (unconditional, clamped): one
+    // round trip, also when the raw frame is read from pinned host memory over PCIe
+    constexpr int NPASS = (PREP_BAND_PIX + PREP_NT - 1) / PREP_NT;
+    float rvs[NPASS];
+#pragma unroll
+    for (int k = 0; k < NPASS; ++k) rvs[k] = a.raw[pbase + min(k * PREP_NT + t, PREP_BAND_PIX - 1)];
+#pragma unroll
+    for (int k = 0; k < NPASS; ++k) {
+        const int p0 = k * PREP_NT;
         const int q = p0 + t, pix = pbase + q;
         const bool in = q < PREP_BAND_PIX;
-        const float rv = rnext;
-        if (q + PREP_NT < PREP_BAND_PIX) rnext = a.raw[pix + PREP_NT];
+        const float rv = rvs[k];
         const double Z = a.to_cm ? (double)rv / 10. : (double)rv;
         if (in) a.depth_cm[pix] = Z;
         const bool nz = in && Z != 0;
@@ -283,21 +295,33 @@ __device__ __forceinline__ void prep_dt(const PrepArgs &a, unsigned char *lds) {
     unsigned *msk = (unsigned *)(lds + PREP_CH * 8 + 64 + 2 * (PREP_NT / 64) * 4);
     float *wmaxp = (float *)(msk + W * H / 32);
     const int t = threadIdx.x, l = t & 63;
-    // hand = non-zero raw depth: 150 pixels per thread, loads issued 30 at a time
-    // (unconditional: no branch splits them into one round trip each)
-    constexpr int NPT = W * H / PREP_NT, B = 30;
-    static_assert(W * H % PREP_NT == 0 && NPT % B == 0, "whole batches");
-    for (int k0 = 0; k0 < NPT; k0 += B) {
-        float v[B];
+    // hand = non-zero raw depth: 150 pixels per thread in three batches of 50 loads, the
+    // next batch in flight while one is folded (unconditional: no branch splits them into
+    // one round trip each; the raw frame may sit in pinned host memory, behind PCIe)
+    constexpr int NPT = W * H / PREP_NT, B = NPT / 3;  // 150 pixels per thread, 3 batches
+    static_assert(W * H % PREP_NT == 0 && NPT % 3 == 0, "whole batches");
+    float va[B], vb[B];
+    auto issue = [&](float (&v)[B], int k0) {
 #pragma unroll
         for (int q = 0; q < B; ++q) v[q] = a.raw[(k0 + q) * PREP_NT + t];
+    };
+    auto fold = [&](const float (&v)[B], int k0) {
 #pragma unroll
         for (int q = 0; q < B; ++q) {
             const unsigned long long bm = __ballot(v[q] != 0.f);
             const int pix = (k0 + q) * PREP_NT + t;
             if ((l & 31) == 0) msk[pix >> 5] = (unsigned)(bm >> (l & 32));
         }
-    }
+    };
+    issue(va, 0);
+    issue(vb, B);
+    fold(va, 0);
+    issue(va, 2 * B);  // the third batch lands while the second is folded
+    fold(vb, B);
+    fold(va, 2 * B);
+    // the band workgroups hold their own raw reads until here (a scheduling hint only):
+    // when the frame sits in host memory the DT, the longer chain, gets PCIe to itself
+    if (t == 0) __hip_atomic_store(&a.ctr[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int *rfirst = (int *)(msk + W * H / 32 + 1);
     if (t == 0) {
         msk[W * H / 32] = 0u;  // the two-word window of the last pixels
@@ -469,7 +493,10 @@ __device__ __forceinline__ void prep_workgroup(const PrepArgs &a, int g, unsigne
     } else {
         prep_dt(a, lds);
     }
-    if (prep_arrive_last(a.ctr + 1, 2, flag) && threadIdx.x == 0) prep_write_descriptor(a);
+    if (prep_arrive_last(a.ctr + 1, 2, flag) && threadIdx.x == 0) {
+        prep_write_descriptor(a);
+        a.ctr[2] = 0u;  // every band is past its wait: ready for the next frame
+    }
 }
 
 __global__ __launch_bounds__(PREP_NT) void k_prepare(PrepArgs a) {
