@@ -58,6 +58,23 @@ __device__ unsigned long long hpe_blk_ts[BT_GENS * BT_BLK * BT_PTS];
     do {             \
     } while (0)
 #endif
+// Refine timeline (diagnostic build only): thread 0 of workgroup 0 appends
+// (s_memrealtime << 8 | phase) at phase boundaries, the count kept in LDS.
+#define RT_LOG 16384
+#if HPE_STAMPS
+__device__ unsigned long long hpe_ref_ts[RT_LOG];
+#define REF_TS(cnt, ph)                                                                    \
+    do {                                                                                   \
+        if (threadIdx.x == 0 && blockIdx.x == 0) {                                         \
+            const unsigned k_ = (cnt)++;                                                   \
+            if (k_ < RT_LOG) hpe_ref_ts[k_] = (__builtin_amdgcn_s_memrealtime() << 8) | (ph); \
+        }                                                                                  \
+    } while (0)
+#else
+#define REF_TS(cnt, ph) \
+    do {                \
+    } while (0)
+#endif
 struct StampClock {
     unsigned long long t, t0 = 0, r0 = 0;
     // whole-kernel span of block 0: shader cycles into slot k, 100 MHz ticks into k + 1

@@ -734,6 +734,7 @@ struct __align__(16) RefineSm {
     double x0[32], g[32], p[32];
     double f[RF_NW];
     FkX X;  // rotation-only joint terms of x0 (refine block 2: translation steps)
+    unsigned ts_n;  // diagnostic build: refine timeline entries written
 };
 
 // Goldstein bracket update (PSO.cpp:459-474), shared by the speculating waves and the walk.
@@ -1006,6 +1007,7 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
             if (f_acc) *f_acc = rs.f[accepted];
         }
         __syncthreads();
+        REF_TS(rs.ts_n, 4);
         sc.lap(19);  // one speculated round
     }
     evals += it;
@@ -1075,6 +1077,8 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
     }
     if constexpr (!STAGED) cv = obs_cloud(o);
     if (t < HPE_DOF) rs.x0[t] = x0g[t];
+    if (t == 0) rs.ts_n = 0;
+    REF_TS(rs.ts_n, 0);
     __shared__ int mwflag;
     MwLeader ml{mw, 0u, false};
     __syncthreads();
@@ -1112,8 +1116,10 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
                 }
                 __syncthreads();
             }
+            REF_TS(rs.ts_n, 1);
             const double fk = eval_corr<MW>(rs, o, cv, H, match, &ml, &mwflag);
             ++evals;
+            REF_TS(rs.ts_n, 2);
             sc.lap(20);
             // cal_grad: x0 +/- e along the 3 block dims, one wave per evaluation
             if (w < 6) {
@@ -1131,6 +1137,7 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
                 rs.p[t] = -1 * g;
             }
             __syncthreads();
+            REF_TS(rs.ts_n, 3);
             sc.lap(21);
             double v1 = 0, v2 = 0;  // op_dot::direct_dot_arma (two accumulators)
             for (int a = 0, b = 1; b < HPE_DOF; a += 2, b += 2) {
@@ -1155,10 +1162,12 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
             if (t < HPE_DOF) rs.x0[t] = rs.x0[t] - tk * rs.g[t];
             base_valid = true;  // accepted node copied, or tk == 0 and x0 unchanged
             __syncthreads();
+            REF_TS(rs.ts_n, 5);
             sc.lap(23);
         }
     }
     if (MW) mw_publish(ml, rs, MW_JOB_EXIT, 0);
+    REF_TS(rs.ts_n, 7);
     if (t < HPE_DOF) x0g[t] = rs.x0[t];
     if (t == 0 && evals_out) *evals_out = evals;
 }
@@ -1205,6 +1214,17 @@ extern "C" int hpe_debug_blk_ts(unsigned long long *out) {
         return HPE_E_HIP;
     std::vector<unsigned long long> z(BT_GENS * BT_BLK * BT_PTS, 0ull);
     if (hipMemcpyToSymbol(HIP_SYMBOL(hpe_blk_ts), z.data(), nb, 0, hipMemcpyHostToDevice) != hipSuccess)
+        return HPE_E_HIP;
+    return HPE_OK;
+}
+// Diagnostic build only: the refine timeline of the last frame, then cleared.
+extern "C" int hpe_debug_ref_ts(unsigned long long *out) {
+    if (!out) return HPE_E_ARG;
+    const size_t nb = sizeof(unsigned long long) * RT_LOG;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hpe_ref_ts), nb, 0, hipMemcpyDeviceToHost) != hipSuccess)
+        return HPE_E_HIP;
+    std::vector<unsigned long long> z(RT_LOG, 0ull);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(hpe_ref_ts), z.data(), nb, 0, hipMemcpyHostToDevice) != hipSuccess)
         return HPE_E_HIP;
     return HPE_OK;
 }
