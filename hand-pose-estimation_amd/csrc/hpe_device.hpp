@@ -75,18 +75,24 @@ __device__ unsigned long long hpe_ref_ts[RT_LOG];
     do {                \
     } while (0)
 #endif
+// HPE_NO_LAPS: a diagnostic build with the wall-clock logs (BLK_TS, WAVE_TS, REF_TS) but
+// without the per-phase cycle laps below, whose global read-modify-writes on thread 0 of
+// block 0 would stretch the phases being timed.
+#ifndef HPE_NO_LAPS
+#define HPE_NO_LAPS 0
+#endif
 struct StampClock {
     unsigned long long t, t0 = 0, r0 = 0;
     // whole-kernel span of block 0: shader cycles into slot k, 100 MHz ticks into k + 1
     __device__ __forceinline__ void begin() {
-        if (HPE_STAMPS && blockIdx.x == 0 && threadIdx.x == 0) {
+        if (HPE_STAMPS && !HPE_NO_LAPS && blockIdx.x == 0 && threadIdx.x == 0) {
             t0 = __builtin_amdgcn_s_memtime();
             r0 = __builtin_amdgcn_s_memrealtime();
             t = t0;
         }
     }
     __device__ __forceinline__ void span(int k) {
-        if (HPE_STAMPS && blockIdx.x == 0 && threadIdx.x == 0) {
+        if (HPE_STAMPS && !HPE_NO_LAPS && blockIdx.x == 0 && threadIdx.x == 0) {
             hpe_stamps[k] += __builtin_amdgcn_s_memtime() - t0;
             hpe_stamps[k + 1] += __builtin_amdgcn_s_memrealtime() - r0;
             hpe_stamps[32 + k] += 1;
@@ -94,10 +100,10 @@ struct StampClock {
         }
     }
     __device__ __forceinline__ void start() {
-        if (HPE_STAMPS && blockIdx.x == 0 && threadIdx.x == 0) t = __builtin_amdgcn_s_memtime();
+        if (HPE_STAMPS && !HPE_NO_LAPS && blockIdx.x == 0 && threadIdx.x == 0) t = __builtin_amdgcn_s_memtime();
     }
     __device__ __forceinline__ void lap(int k) {
-        if (HPE_STAMPS && blockIdx.x == 0 && threadIdx.x == 0) {
+        if (HPE_STAMPS && !HPE_NO_LAPS && blockIdx.x == 0 && threadIdx.x == 0) {
             const unsigned long long n = __builtin_amdgcn_s_memtime();
             hpe_stamps[k] += n - t;
             hpe_stamps[32 + k] += 1;

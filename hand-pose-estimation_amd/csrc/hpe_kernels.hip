@@ -835,7 +835,9 @@ __device__ __forceinline__ void eval_nodes(RefineSm &rs, int nn, const DevObs &o
             const double f = eval_wave_frozen(rs.w[w], o, cv, H, match, Xt);
             if (l == 0) rs.f[w] = f;
         }
+        REF_TS(rs.ts_n, 9);  // wave 0's node done
         __syncthreads();
+        REF_TS(rs.ts_n, 8);  // every node done
         return;
     }
     mw_publish(*ml, rs, MW_JOB_FROZEN, nn);

@@ -1,5 +1,5 @@
-"""Diagnostic: per-block wall-clock phases of k_pso_gen from the stamps build
-(libhpe_stamps.so, s_memrealtime at 100 MHz).  Tracks a few pipelined frames and
+"""Diagnostic: per-block wall-clock phases of k_pso_gen from the timelines build
+(libhpe_rts.so, s_memrealtime at 100 MHz).  Tracks a few pipelined frames and
 analyses the generations of the last one.  Usage: python tools/blk_ts.py [frames] [P]"""
 import ctypes as C
 import sys
@@ -14,7 +14,7 @@ sys.path.insert(0, str(ROOT / "hand-pose-estimation_amd"))
 import hpe  # noqa: E402
 from hpe import _lib, synth  # noqa: E402
 
-lib = _lib.load(ROOT / "hand-pose-estimation_amd" / "libhpe_stamps.so")
+lib = _lib.load(ROOT / "hand-pose-estimation_amd" / "libhpe_rts.so")  # make timelines
 _lib._lib = lib
 lib.hpe_debug_blk_ts.restype = C.c_int
 lib.hpe_debug_blk_ts.argtypes = [C.POINTER(C.c_uint64)]

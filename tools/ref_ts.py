@@ -1,5 +1,5 @@
 """Diagnostic: wall-clock timeline of refine_init_pose (k_refine workgroup 0) from the
-stamps build (libhpe_stamps.so, s_memrealtime at 100 MHz), over pipelined frames.
+timelines build (libhpe_rts.so, s_memrealtime at 100 MHz), over pipelined frames.
 Phases: corr = cal_cost2 with new correspondences, grad = the six central differences,
 gold = one speculated Goldstein round, glue = the rest of an iteration.
 Usage: python tools/ref_ts.py [frames] [P]"""
@@ -17,7 +17,7 @@ sys.path.insert(0, str(ROOT / "hand-pose-estimation_amd"))
 import hpe  # noqa: E402
 from hpe import _lib, synth  # noqa: E402
 
-lib = _lib.load(ROOT / "hand-pose-estimation_amd" / "libhpe_stamps.so")
+lib = _lib.load(ROOT / "hand-pose-estimation_amd" / "libhpe_rts.so")  # make timelines
 _lib._lib = lib
 lib.hpe_debug_ref_ts.restype = C.c_int
 lib.hpe_debug_ref_ts.argtypes = [C.POINTER(C.c_uint64)]
@@ -46,21 +46,30 @@ for f in range(nfr + 3):
     ent = [(int(v) >> 8, int(v) & 0xff) for v in buf if v]
     if not ent:
         continue
-    t_prev, ph_prev = ent[0]
+    last = {}
     iters = rounds = 0
-    for t, ph in ent[1:]:
-        d = (t - t_prev) / 100.0  # us
-        if ph == 2:
-            dur["corr"].append(d); iters += 1
+    rstart = None  # start of the current batch of node evaluations
+    for t, ph in ent:
+        if ph == 1:
+            if 0 in last and iters == 0:
+                dur["start"].append((t - last[0]) / 100.0)
+        elif ph == 2:
+            dur["corr"].append((t - last[1]) / 100.0); iters += 1
+            rstart = t
+        elif ph == 9:
+            dur["  node0 eval"].append((t - rstart) / 100.0)
+        elif ph == 8:
+            dur["  barrier wait"].append((t - last[9]) / 100.0)
         elif ph == 3:
-            dur["grad"].append(d)
+            dur["grad"].append((t - last[2]) / 100.0)
+            rstart = t
         elif ph == 4:
-            dur["gold round"].append(d); rounds += 1
+            dur["gold round"].append((t - rstart) / 100.0); rounds += 1
+            dur["  walk+copy"].append((t - last[8]) / 100.0)
+            rstart = t
         elif ph == 5:
-            dur["glue"].append(d)
-        elif ph == 1 and ph_prev == 0:
-            dur["start"].append(d)
-        t_prev, ph_prev = t, ph
+            dur["glue"].append((t - last[4]) / 100.0 if 4 in last else 0.0)
+        last[ph] = t
     per_frame.append(((ent[-1][0] - ent[0][0]) / 100.0, iters, rounds))
 for k, v in dur.items():
     v = np.array(v)
