@@ -31,7 +31,14 @@ def _frames(np_hand):
     edge = e.copy(); edge[0:6, 0:9] = 250.0; edge[-4:, -7:] = 251.0; edge[120, :] = 260.0
     rng = np.random.default_rng(1)
     speck = np.where(rng.random((240, 320)) < 0.02, rng.uniform(200, 600, (240, 320)), 0).astype(np.float32)
-    return out + [e, one, full, edge, speck]
+    # the DT's forward scan starts at the first row holding a hand pixel (an even row at
+    # or above it): first hand rows odd / even / last, a lone pixel in a corner column
+    late = []
+    for r, c in ((1, 5), (133, 160), (238, 0), (239, 319), (239, 0), (200, 319)):
+        x = e.copy(); x[r, c] = 321.0
+        late.append(x)
+    band = e.copy(); band[133:140, 40:90] = 410.0; band[201, 300:320] = 415.0
+    return out + [e, one, full, edge, speck, band] + late
 
 
 def _check(a, b):
