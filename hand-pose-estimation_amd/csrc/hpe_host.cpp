@@ -195,8 +195,9 @@ void make_normals(uint64_t seed, int P, double *out, uint32_t stream) {
 // Topology of generation t (PSO.cpp:790-803): each particle s links to
 // r = floor(u*(P-1) + 0.5) for 3 draws; receiver r's informants are {r} U {s -> r}.
 // outl[t][s][k] = (r, slot of s in r's ascending source list); K = max in-degree.
-int make_links(uint64_t seed, int P, int G, std::vector<int> &outl) {
+int make_links(uint64_t seed, int P, int G, std::vector<int> &outl, std::vector<int> *indeg) {
     outl.assign((size_t)(G + 1) * P * 6, -1);
+    if (indeg) indeg->assign((size_t)(G + 1) * P, 0);
     std::vector<int> fill(P);
     int K = 1;
     for (int t = 1; t <= G; ++t) {
@@ -210,6 +211,7 @@ int make_links(uint64_t seed, int P, int G, std::vector<int> &outl) {
                 o[1] = fill[r]++;
                 K = std::max(K, fill[r]);
             }
+        if (indeg) std::copy(fill.begin(), fill.end(), indeg->begin() + (size_t)t * P);
     }
     return K;
 }

@@ -16,5 +16,7 @@ int preprocess_depth(const float *depth_mm, int to_cm, int downsample, double fo
                      double *scale_out, double *dtmax_out, double K[9]);
 double host_u01(uint64_t seed, uint32_t stream, uint32_t gen, uint32_t idx, uint32_t k);
 void make_normals(uint64_t seed, int P, double *out, uint32_t stream = ST_NORMAL);
-int make_links(uint64_t seed, int P, int G, std::vector<int> &outl);
+// links of every topology 1..G; indeg (optional): (G+1) x P in-degree per topology
+int make_links(uint64_t seed, int P, int G, std::vector<int> &outl,
+               std::vector<int> *indeg = nullptr);
 }  // namespace hpe

@@ -252,7 +252,8 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_init(DevSwarm sw, const double *
 // only.  Waves 1..3 prefetch the push links meanwhile; then all 8 waves search.
 __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *__restrict__ og,
                                                     const DevHand *__restrict__ Hg, int g,
-                                                    double W1, double C1, double C2) {
+                                                    double W1, double C1, double C2,
+                                                    InboxCounts kin) {
     BLK_TS(g, 0);
     StampClock sc;
     sc.begin();
@@ -260,6 +261,8 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
     __shared__ Smem sm;
     __shared__ double ib[2][IB_KMAX][IB_FIELDS];
     const int i = blockIdx.x, t = threadIdx.x, P = sw.P, K = sw.K;
+    // valid slots of this receiver's kept (0) / rebuilt (1) inbox: only these are read
+    const int k0 = (P <= KIN_MAX) ? kin.k0[i] : K, k1 = (P <= KIN_MAX) ? kin.k1[i] : K;
     // Round 1: every load of the generation is issued before any value is used (one
     // memory round trip): hand words, first cloud point, push links, inbox payload rows
     // (waves 1..7); own state, own pbest cost, inbox tags / costs, gmin cells, sig (wave 0).
@@ -276,15 +279,16 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
     int inf = 0, islot = -1, var = 0;
     if (t >= 64) {
         // ---- waves 1..7: both informant inboxes (payload rows) into LDS
+        // the k0 valid kept slots, then the k1 valid rebuilt ones
         const double *src = sw.inbox + ib_index(sw, (g - 1) & 1, 0, i, 0);
         const size_t var_stride = (size_t)P * K * IB_FIELDS;
-        const int n = 2 * K * IB_FIELDS, u0 = t - 64;
+        const int n = (k0 + k1) * IB_FIELDS, u0 = t - 64;
         double a[3];
 #pragma unroll
         for (int k = 0; k < 3; ++k) {  // unconditional (clamped) loads: no early wait
-            const int u = min(u0 + k * (HPE_NT - 64), n - 1);
-            const int vr = u >= K * IB_FIELDS ? 1 : 0;
-            a[k] = src[vr * var_stride + (u - vr * K * IB_FIELDS)];
+            const int u = min(u0 + k * (HPE_NT - 64), max(n - 1, 0));
+            const int vr = u >= k0 * IB_FIELDS ? 1 : 0;
+            a[k] = src[vr * var_stride + (u - vr * k0 * IB_FIELDS)];
         }
         if (t < 64 + 2 * HPE_DOF) {  // wave 1 draws rp, rg while the loads are in flight
             const int j = t - 64, d = j < HPE_DOF ? j : j - HPE_DOF;
@@ -293,7 +297,7 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             const int u = u0 + k * (HPE_NT - 64);
-            if (u < n) (&ib[0][0][0])[(u >= K * IB_FIELDS ? IB_KMAX * IB_FIELDS - K * IB_FIELDS : 0) + u] = a[k];
+            if (u < n) (&ib[0][0][0])[(u >= k0 * IB_FIELDS ? IB_KMAX * IB_FIELDS - k0 * IB_FIELDS : 0) + u] = a[k];
         }
     } else {
         // ---- wave 0, round 1: own state, gbest bookkeeping, inbox tags / costs
@@ -307,7 +311,8 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
         double tg[2], tc[2];
 #pragma unroll
         for (int vr = 0; vr < 2; ++vr) {
-            const double *sl = sw.inbox + ib_index(sw, (g - 1) & 1, vr, i, t < K ? t : K - 1);
+            const int kv = vr ? k1 : k0;
+            const double *sl = sw.inbox + ib_index(sw, (g - 1) & 1, vr, i, min(t, max(kv - 1, 0)));
             tg[vr] = sl[0];
             tc[vr] = sl[1];
         }
@@ -342,7 +347,7 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
         const int self_lane = (K <= 15) ? 15 : 63;
         double v = __builtin_inf();
         int idx = 0x7fffffff, slot = -1;
-        if (t < K) {
+        if (t < (var ? k1 : k0)) {
             const long long tag = __double_as_longlong(var ? tg[1] : tg[0]);
             if ((tag >> 32) == (((long long)(g - 1) << 16) | topo)) {
                 v = var ? tc[1] : tc[0];

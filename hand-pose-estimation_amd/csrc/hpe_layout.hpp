@@ -77,6 +77,18 @@ struct DevSwarm {
     int P, G, K;
 };
 
+// Valid inbox slots per receiver for ONE generation g of the workgroup form, passed in the
+// kernel arguments (read with the other argument words, no dependent round trip).  Slots
+// of a topology are filled from 0 (hpe::make_links), so receiver i reads only
+// k1[i] = in-degree of i under topology g (rebuilt variant) and k0[i] = the largest
+// in-degree of i under any topology 1..g-1 (kept variant), instead of K (the maximum over
+// all receivers and topologies) in both.  Swarms above KIN_MAX receivers read K.
+#define KIN_MAX 1024
+struct InboxCounts {
+    uint8_t k0[KIN_MAX];
+    uint8_t k1[KIN_MAX];
+};
+
 
 // pso_optimise state (PSO.cpp:539-712): global-best PSO whose particles first take ten
 // single-coordinate Goldstein steps each generation.  The gbest position is needed by the
