@@ -319,6 +319,25 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
         const unsigned long long gcell = gmin_load(sw, g - 1);
         const Sig pv = sw.sig[g > 1 ? g - 1 : 0];
         const double fmin = gmin_reduce(gcell);  // NaN when no value was written
+        // informant = first argmin of pbest cost over {i} U incoming (PSO.cpp:810-812),
+        // under BOTH variants while the gmin reduction is in flight (independent chains):
+        // rebuilt = topology g, kept = the topology of g-1 (pv.topo); the decision below
+        // only selects.  Candidates in lanes 0..k-1, self in lane 15 (K <= 15: one 16-lane
+        // row) or 63.
+        const int self_lane = (K <= 15) ? 15 : 63;
+        int infv[2], islv[2];
+#pragma unroll
+        for (int vr = 0; vr < 2; ++vr) {
+            const long long tag = __double_as_longlong(tg[vr]);
+            const int tt = vr ? g : pv.topo;
+            const bool ok = t < (vr ? k1 : k0) && (tag >> 32) == (((long long)(g - 1) << 16) | tt);
+            const bool self = t == self_lane;  // L = eye
+            double v = ok ? tc[vr] : (self ? pci : __builtin_inf());
+            const int idx = ok ? (int)(tag & 0xffffffff) : (self ? i : 0x7fffffff);
+            if (v != v) v = __builtin_inf();
+            if (K <= 15) row0_argmin_lex(v, idx, ok ? t : -1, infv[vr], islv[vr]);
+            else wave_argmin_lex(v, idx, ok ? t : -1, infv[vr], islv[vr]);
+        }
         BLK_TS(g, 6);
         // end-of-generation update of g-1 (PSO.cpp:864-877) / initial gbest (:755-760),
         // computed redundantly by every lane (uniform values)
@@ -339,28 +358,11 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
             sm.iscal[0] = sg.topo;
             sm.dscal[4] = pci;
         }
-        const int topo = sg.topo;
-        var = (topo == g) ? 1 : 0;
+        // var 1 iff topology g is in use; otherwise (count == 0, g >= 2) it is pv.topo
+        var = (sg.topo == g) ? 1 : 0;
         sc.lap(0);
-        // informant = first argmin of pbest cost over {i} U incoming (PSO.cpp:810-812)
-        // candidates in lanes 0..K-1, self in lane 15 (K <= 15: one 16-lane row) or 63
-        const int self_lane = (K <= 15) ? 15 : 63;
-        double v = __builtin_inf();
-        int idx = 0x7fffffff, slot = -1;
-        if (t < (var ? k1 : k0)) {
-            const long long tag = __double_as_longlong(var ? tg[1] : tg[0]);
-            if ((tag >> 32) == (((long long)(g - 1) << 16) | topo)) {
-                v = var ? tc[1] : tc[0];
-                idx = (int)(tag & 0xffffffff);
-                slot = t;
-            }
-        } else if (t == self_lane) {  // self (L = eye)
-            v = pci;
-            idx = i;
-        }
-        if (v != v) v = __builtin_inf();
-        if (K <= 15) row0_argmin_lex(v, idx, slot, inf, islot);
-        else wave_argmin_lex(v, idx, slot, inf, islot);
+        inf = var ? infv[1] : infv[0];
+        islot = var ? islv[1] : islv[0];
         BLK_TS(g, 7);
         sc.lap(1);
     }
