@@ -526,14 +526,16 @@ __device__ __forceinline__ float hi_sqrt_class(float m) {
     return h;
 }
 
-// key = j if (bits(d2) <= hb) else j + 64, as three plain VALU ops (the compiler would
-// otherwise rebuild it as v_cmp + v_cndmask through VCC, one s_nop hazard each).
+// key = j if (bits(d2) <= hb) else j | 2^31 (unsigned order: the first j at or below hb
+// is the minimum key), as two plain VALU ops: the sign bit of hb - bits(d2) masked in
+// over j (the compiler would otherwise rebuild it as v_cmp + v_cndmask through VCC, one
+// s_nop hazard each).  For non-negative floats the sign bit is exactly bits(d2) > hb.
 template <int J>
-__device__ __forceinline__ int sqrt_class_key(int hb, float d2) {
-    int k;
-    asm("v_sub_u32 %0, %1, %2\n\tv_lshrrev_b32 %0, 31, %0\n\tv_lshl_or_b32 %0, %0, 6, %3"
+__device__ __forceinline__ unsigned sqrt_class_key(int hb, float d2) {
+    unsigned k;
+    asm("v_sub_u32 %0, %1, %2\n\tv_and_or_b32 %0, %0, %3, %4"
         : "=&v"(k)
-        : "v"(hb), "v"(__float_as_int(d2)), "i"(J));
+        : "v"(hb), "v"(__float_as_int(d2)), "s"(0x80000000u), "i"(J));
     return k;
 }
 
@@ -584,11 +586,11 @@ __device__ __forceinline__ double search_align(const FkSm &f, const CV &cv,
         BLK_TS(g_ts, 11);
         m = fminf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0xB1, 0xf, 0xf,
                                                                false)));  // partner lane t^1
-        // first j with bits(d2[j]) <= hb, branch-free: key_j = j, or j + 64 when
+        // first j with bits(d2[j]) <= hb, branch-free: key_j = j, or j | 2^31 when
         // d2[j] > hb (non-negative floats order like their bit patterns), then an
-        // integer min tree and the partner lane's half
+        // unsigned min tree and the partner lane's half
         auto first_le = [&](int hb) {
-            int key[24];
+            unsigned key[24];
 #define HPE_KEY(J) key[J] = sqrt_class_key<J>(hb, d2[J]);
             HPE_KEY(0) HPE_KEY(1) HPE_KEY(2) HPE_KEY(3) HPE_KEY(4) HPE_KEY(5) HPE_KEY(6) HPE_KEY(7)
             HPE_KEY(8) HPE_KEY(9) HPE_KEY(10) HPE_KEY(11) HPE_KEY(12) HPE_KEY(13) HPE_KEY(14)
@@ -597,9 +599,9 @@ __device__ __forceinline__ double search_align(const FkSm &f, const CV &cv,
 #undef HPE_KEY
 #pragma unroll
             for (int j = 0; j < 24; j += 3) key[j] = min(min(key[j], key[j + 1]), key[j + 2]);
-            int ix = min(min(min(key[0], key[3]), min(key[6], key[9])),
-                         min(min(key[12], key[15]), min(key[18], key[21])));
-            ix = (ix >= 64) ? (1 << 20) : ix + 24 * h;
+            const unsigned kx = min(min(min(key[0], key[3]), min(key[6], key[9])),
+                                    min(min(key[12], key[15]), min(key[18], key[21])));
+            const int ix = (kx >= 64u) ? (1 << 20) : (int)kx + 24 * h;
             return min(ix, __builtin_amdgcn_mov_dpp(ix, 0xB1, 0xf, 0xf, false));
         };
         // BFMatcher's match is the first j with d2[j] <= hi = hi_sqrt_class(m) (the sqrt
