@@ -581,7 +581,13 @@ __device__ __forceinline__ double search_align(const FkSm &f, const CV &cv,
             const f2 d = (t0 * t0 + t1 * t1) + t2 * t2;
             d2[j] = d.x;
             d2[j + 1] = d.y;
-            m = fminf(m, fminf(d.x, d.y));
+        }
+        {  // minimum as a three-level tree of 3-way mins (v_min3_f32), not a 12-deep chain
+            float m3[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) m3[k] = fminf(fminf(d2[3 * k], d2[3 * k + 1]), d2[3 * k + 2]);
+            m = fminf(fminf(fminf(m3[0], m3[1]), m3[2]), fminf(fminf(m3[3], m3[4]), m3[5]));
+            m = fminf(m, fminf(m3[6], m3[7]));
         }
         BLK_TS(g_ts, 11);
         m = fminf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0xB1, 0xf, 0xf,
