@@ -351,3 +351,29 @@ def test_pso_evolve_wave_form(oracle, ora_hand, np_hand, P, maxiter, monkeypatch
     g, cnt, topo = pso.trace(cf)
     np.testing.assert_allclose(g, tr["gbest"], rtol=1e-8)
     assert np.array_equal(cnt, tr["count"]) and np.array_equal(topo, tr["topo"])
+
+
+@pytest.mark.parametrize("P,maxiter", [(1024, 4), (1030, 3)])
+def test_pso_evolve_block_form_inbox_counts(oracle, ora_hand, np_hand, P, maxiter, monkeypatch):
+    """The workgroup-per-particle generation kernel at the edge of its per-receiver inbox
+    counts (InboxCounts in the kernel arguments, P <= KIN_MAX = 1024) and just above it
+    (every receiver reads the K slots of both variants), against the oracle."""
+    import hpe
+    monkeypatch.setenv("HPE_PSO_FORM", "block")
+    gh = hpe.reference_hand(device=0)  # context created with the block form forced
+    truth = hand_data.trajectory(2, seed=5)[1]
+    d = oracle_np.render_depth_mm(np_hand, truth)
+    obs, om = _obs_pair(oracle, gh, d)
+    cf = hpe.costfunc(gh, om)
+    ub, lb, sd = oracle_np.reference_bounds()
+    pso = hpe.PSO()
+    pso.set_pso_params(ub, lb, sd, 0.7298, 1.49618, 1.49618, maxiter, 1e-8, 1e-8)
+    bestp = np.zeros(26)
+    x0 = oracle_np.X0.copy()
+    assert pso.pso_evolve(cf, x0, P, bestp) == 1
+    rb, rc, tr = oracle.pso_evolve(ora_hand, obs, x0, P, maxiter, lb, ub, sd, seed=1000)
+    np.testing.assert_allclose(bestp, rb, rtol=0, atol=1e-6)
+    assert abs(pso.last_gbest_cost - rc) <= 1e-8 * abs(rc)
+    g, cnt, topo = pso.trace(cf)
+    np.testing.assert_allclose(g, tr["gbest"], rtol=1e-8)
+    assert np.array_equal(cnt, tr["count"]) and np.array_equal(topo, tr["topo"])
