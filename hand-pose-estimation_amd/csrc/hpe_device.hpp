@@ -129,6 +129,7 @@ struct __align__(16) Smem {
     double dscal[8];
     int iscal[16];
     double draws[2 * HPE_DOF];  // rp, rg of the generation (k_pso_gen)
+    double pbr[32];             // own pbest row at entry (k_pso_gen's pushes)
 };
 
 // Global-memory pointers.  Pointers read from memory (the frame descriptor DevObs) are

@@ -363,6 +363,7 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
         sc.lap(0);
         inf = var ? infv[1] : infv[0];
         islot = var ? islv[1] : islv[0];
+        if (t < HPE_DOF) sm.pbr[t] = pbi;  // for the pushing waves, if x does not improve
         BLK_TS(g, 7);
         sc.lap(1);
     }
@@ -406,17 +407,16 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
     sc.start();
     const bool better = fx < pci;
     const double pn = better ? fx : pci;
-    if (t < HPE_DOF) {
-        const double row = better ? sm.fk.th[t] : pbi;
-        sw.pb[e] = row;
-        sm.fk.th[t] = row;  // the pushed pbest row
-    }
+    if (t < HPE_DOF) sw.pb[e] = better ? sm.fk.th[t] : pbi;
     if (t == 0) {
         sw.pch[(size_t)g * P + i] = pn;
         gmin_lower(sw, g, i, pn);
     }
-    __syncthreads();
-    push_inbox(sw, g, i, q, q < 3 * IB_FIELDS ? lk1 : lk0, q < 3 * IB_FIELDS ? g + 1 : topo, pn, sm.fk.th);
+    // the pushed pbest row: this generation's x (in LDS since the velocity step) or the
+    // entry pbest (staged before the first barrier); `better` is block-uniform, so no
+    // barrier waits for wave 0 here
+    push_inbox(sw, g, i, q, q < 3 * IB_FIELDS ? lk1 : lk0, q < 3 * IB_FIELDS ? g + 1 : topo, pn,
+               better ? sm.fk.th : sm.pbr);
     BLK_TS(g, 5);
     sc.lap(3);
     sc.span(5);
