@@ -15,15 +15,26 @@ N = 250 cloud points (the reference's downsample=true default; --full-cloud: all
   multi-GPU    = one process per GPU, independent subswarms (seed 1000+rank) with one
                  RCCL all-gather of {bestp, cost} per frame; weak scaling
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-       (N > 1 is launched by torch.distributed.run, one rank per GPU)
+--config selects a BASELINE.json workload: seq (default; configs[1]/[2]: 256 x 30 tracked
+frames), p32 (configs[0]'s shape, 32 x 10), p4096 (configs[3], 4096 x 40), subswarm8
+(configs[4]: 1024 particles per rank x 30; run with --gpus 8).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config NAME]
+       --gpus N > 1 without a torch.distributed environment re-launches itself under
+       `python -m torch.distributed.run --nproc-per-node N` (a child process started
+       before anything touches the GPU) and exits with its return code.
+       --stub: no GPU -- each rank exchanges a stub tracker state over gloo (CPU test of
+       the launcher and the exchange).
 """
 from __future__ import annotations
 
 import argparse
 import ctypes as C
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -34,12 +45,20 @@ sys.path.insert(0, str(ROOT / "hand-pose-estimation_amd"))
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
 FP32_PEAK_TFLOPS = 157.3  # vector fp32 (spec); the search is fp32 VALU, no MFMA
 
+CONFIGS = {  # name -> (particles, generations, BASELINE.json workload)
+    "seq": (256, 30, "configs[1]/[2]: tracked sequence, 256 particles x 30 generations, "
+                     "refine + temporal prior"),
+    "p32": (32, 10, "configs[0]'s shape on the GPU: 32 particles x 10 generations"),
+    "p4096": (4096, 40, "configs[3]: large swarm, 4096 particles x 40 generations"),
+    "subswarm8": (1024, 30, "configs[4]: 1024-particle subswarm per rank x 30 generations, "
+                            "all-gather of the best per frame"),
+}
+
 
 def algorithmic_bytes_per_eval(n: int) -> int:
-    # cloud xyz fp64 (24 B/pt) + 48 x (depth fp64 + DT fp32) gathers
-    # + PSO state: read x, v, pbest, pbest[informant]; write x, v, pbest (7 x 26 fp64)
-    # + pcost read/write (16 B)                                       
-    return 24 * n + 48 * 12 + 7 * 26 * 8 + 16
+    # SURVEY.md §8 d2 / BASELINE.md §3: fp32 xyz cloud (12 B/pt) + 48 x (depth + DT)
+    # gathers (384 B) + theta (208 B) + cost (8 B) = 12N + 600
+    return 12 * n + 600
 
 
 def algorithmic_flops_per_eval(n: int) -> int:
@@ -53,78 +72,118 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--particles", type=int, default=256)
-    ap.add_argument("--generations", type=int, default=30)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="seq")
+    ap.add_argument("--particles", type=int, default=None, help="override the config's P")
+    ap.add_argument("--generations", type=int, default=None, help="override the config's G")
     ap.add_argument("--full-cloud", action="store_true", help="no down-sampling (N ~ 9.3k)")
     ap.add_argument("--no-refine", action="store_true")
     ap.add_argument("--resident", action="store_true",
                     help="preprocess every frame before timing (default: each step prepares "
                          "the next frame from host depth on the GPU, overlapped)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--seed", type=int, default=0, help="trajectory seed")
     ap.add_argument("--frames", default=os.environ.get("HPE_FRAMES_DIR"),
                     help="directory of MSRA-style *_depth.bin frames (headerless float32 mm, "
                          "240x320) to track instead of the synthetic sequence")
-    return ap.parse_args()
+    ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)
+    a = ap.parse_args()
+    P, G, _ = CONFIGS[a.config]
+    a.particles = a.particles or P
+    a.generations = a.generations if a.generations is not None else G
+    return a
 
 
-def cpu_baseline(args, sizes_hint, recorded=None):
+# ------------------------------------------------------------------------- launcher
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def relaunch(args) -> int:
+    """--gpus N > 1 from a plain invocation: run this script under torch.distributed.run
+    as a child process (nothing in this process has touched the GPU), relay its output,
+    return its exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           f"--master-port={_free_port()}", str(Path(__file__).resolve())] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+# ------------------------------------------------------------------------- CPU baseline
+def cgroup_cpu_quota():
+    """CPUs granted by the cgroup v2 cpu.max quota (None: unlimited or unknown)."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else max(1, int(round(int(q) / int(per))))
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(args, recorded=None):
     """The oracle (C restatement, OpenMP over particles where the reference has
-    `omp parallel for`) tracking the same synthetic frames on the host: a bounded
-    sample of the same workload."""
+    `omp parallel for`, PSO.cpp:748,848) tracking the same synthetic frames on the host:
+    bounded samples of the same workload.  Threads: the reference's OpenMP default, every
+    CPU of the process's affinity (nproc); also at the cgroup CPU quota
+    when one is set below it (oversubscribed OpenMP barriers stall); the faster leg is
+    the reported value.  Plus a 1-thread leg."""
     sys.path.insert(0, str(ROOT / "oracle"))
-    import numpy as np
     import oracle_c
     import oracle_np
     import hpe
     from hpe import synth
     o = oracle_c.load(build=False)
     d = json.loads((ROOT / "hand-pose-estimation_amd/hpe/hand_subject1.json").read_text())
-    geo, rad = np.array(d["hgeo_mm"]) / 10.0, np.array(d["rad_mm"]) / 10.0
+    geo, rad = d["hgeo_mm"], d["rad_mm"]
+    import numpy as np
+    geo, rad = np.array(geo) / 10.0, np.array(rad) / 10.0
     h = o.hand(geo, rad)
     nh = oracle_np.Hand(geo, rad)
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
     P, G = args.particles, args.generations
     ub, lb, sd = hpe.reference_bounds()
     if recorded is not None:  # the same recorded frames the GPU tracked
-        raw = recorded
-        poses = [hpe.X0.copy()]
+        raw, x_start = recorded, hpe.X0.copy()
     else:
         poses = synth.trajectory(64, args.seed)
         raw = [oracle_np.render_depth_mm(nh, poses[f]) for f in range(len(poses))]
-    x = poses[0].copy()
-    done, t0, n_pts = 0, time.perf_counter(), 0
-    while True:
-        obs = o.preprocess(raw[done % len(raw)], downsample=not args.full_cloud)  # next_frame
-        n_pts = obs.n
-        if not args.no_refine:
-            x, _ = o.refine(h, obs, x)
-        x, _, _ = o.pso_evolve(h, obs, x, P, G + 1, lb, ub, sd, seed=1000, nthreads=threads)
-        o.cal_cost(h, obs, x)
-        done += 1
-        el = time.perf_counter() - t0
-        if el >= args.cpu_seconds or done >= 4096:
-            break
-    out = {"value": P * (G + 1) * done / el, "unit": "particle-evals/s", "cores": threads,
-           "kind": "port", "tracked_fps": done / el,
-           "sample": f"{done} tracked frames incl. preprocessing ({P}p x {G} gen, N={n_pts}, "
-                     f"refine={'off' if args.no_refine else 'on'}) of the same synthetic "
-                     f"sequence in {el:.1f} s, oracle/hpe_oracle.c with {threads} OpenMP threads"}
-    # the single-thread rate of the same loop (SURVEY.md §8 d3), a shorter sample
-    x, done1, t0 = poses[0].copy(), 0, time.perf_counter()
-    while True:
-        obs = o.preprocess(raw[done1 % len(raw)], downsample=not args.full_cloud)
-        if not args.no_refine:
-            x, _ = o.refine(h, obs, x)
-        x, _, _ = o.pso_evolve(h, obs, x, P, G + 1, lb, ub, sd, seed=1000, nthreads=1)
-        o.cal_cost(h, obs, x)
-        done1 += 1
-        el1 = time.perf_counter() - t0
-        if el1 >= args.cpu_seconds / 3 or done1 >= 1024:
-            break
-    out["one_thread"] = {"value": P * (G + 1) * done1 / el1, "tracked_fps": done1 / el1,
-                         "sample": f"{done1} tracked frames in {el1:.1f} s, 1 thread"}
+        x_start = poses[0].copy()
+
+    def leg(threads, seconds, max_frames):
+        x, done, t0, n_pts = x_start.copy(), 0, time.perf_counter(), 0
+        while True:
+            obs = o.preprocess(raw[done % len(raw)], downsample=not args.full_cloud)
+            n_pts = obs.n
+            if not args.no_refine:
+                x, _ = o.refine(h, obs, x)
+            x, _, _ = o.pso_evolve(h, obs, x, P, G + 1, lb, ub, sd, seed=1000, nthreads=threads)
+            o.cal_cost(h, obs, x)
+            done += 1
+            el = time.perf_counter() - t0
+            if el >= seconds or done >= max_frames:
+                return {"value": P * (G + 1) * done / el, "tracked_fps": done / el,
+                        "threads": threads, "frames": done, "seconds": el, "cloud_points": n_pts}
+
+    affinity = len(os.sched_getaffinity(0))
+    quota = cgroup_cpu_quota()
+    legs = {"affinity": leg(affinity, args.cpu_seconds, 4096)}
+    if quota and quota < affinity:
+        legs["cgroup_quota"] = leg(quota, args.cpu_seconds, 4096)
+    best = max(legs.values(), key=lambda r: r["value"])
+    one = leg(1, args.cpu_seconds / 3, 1024)
+    out = {"value": best["value"], "unit": "particle-evals/s", "cores": best["threads"],
+           "kind": "port", "tracked_fps": best["tracked_fps"],
+           "sample": (f"{best['frames']} tracked frames incl. preprocessing ({P}p x {G} gen, "
+                      f"N={best['cloud_points']}, refine={'off' if args.no_refine else 'on'}) "
+                      f"of the same synthetic sequence in {best['seconds']:.1f} s, "
+                      f"oracle/hpe_oracle.c with {best['threads']} OpenMP threads"),
+           "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+           "legs": {k: {kk: v[kk] for kk in ("threads", "value", "tracked_fps", "frames")}
+                    for k, v in legs.items()},
+           "one_thread": {"value": one["value"], "tracked_fps": one["tracked_fps"],
+                          "sample": f"{one['frames']} tracked frames in {one['seconds']:.1f} s, "
+                                    f"1 thread"}}
     try:
         for line in open("/proc/cpuinfo"):
             if line.startswith("model name"):
@@ -135,28 +194,102 @@ def cpu_baseline(args, sizes_hint, recorded=None):
     return out
 
 
-def load_pmc(P, n_points):
-    """HBM traffic per k_pso_gen launch from the committed rocprofv3 --pmc summary."""
-    p = ROOT / "profiles" / "pmc_k_pso_gen.json"
+# ------------------------------------------------------------------------- roofline
+def lib_sha256(path):
+    return hashlib.sha256(Path(path).read_bytes()).hexdigest()
+
+
+def load_pmc(kernel, P, n_points, lib_path):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc summary
+    (profiles/pmc_<kernel>.json), only if it was captured from this very libhpe.so build
+    and workload; otherwise None."""
+    p = ROOT / "profiles" / f"pmc_{kernel}.json"
     if not p.exists():
-        return None
+        return None, "no PMC capture committed"
     try:
         d = json.loads(p.read_text())
-        if d.get("particles") == P and d.get("cloud_points") == n_points:
-            return d.get("bytes_per_launch")
-    except Exception:
+    except ValueError:
+        return None, "unreadable PMC capture"
+    if d.get("lib_sha256") != lib_sha256(lib_path):
+        return None, "PMC capture is of another libhpe.so build"
+    if d.get("particles") != P or d.get("cloud_points") != n_points:
+        return None, "PMC capture is of another workload"
+    return d.get("bytes_per_launch"), f"profiles/pmc_{kernel}.json (same build, sha256 match)"
+
+
+def roofline_entry(kernel, prof, evals_per_launch, n_pts, lib_path, P):
+    k = prof[kernel]
+    if not k["launches"]:
         return None
-    return None
+    avg_s = k["avg_us"] * 1e-6
+    bpl = evals_per_launch * algorithmic_bytes_per_eval(n_pts)
+    fpl = evals_per_launch * algorithmic_flops_per_eval(n_pts)
+    achieved = bpl / avg_s / 1e9
+    traffic, tsrc = load_pmc(kernel, P, n_pts, lib_path)
+    valu = fpl / avg_s / 1e12
+    return {"bound": "hbm", "kernel": kernel, "achieved": achieved, "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "traffic_source": tsrc, "avg_launch_us": k["avg_us"], "launches": k["launches"],
+            "evals_per_launch": evals_per_launch, "bytes_per_launch": bpl,
+            "flops_per_launch": fpl, "valu_tflops": valu, "valu_frac": valu / FP32_PEAK_TFLOPS}
 
 
+# ------------------------------------------------------------------------- stub ranks
+def stub_main(args, world, rank):
+    """CPU rehearsal of the multi-rank path: gloo, each rank a stub tracker state whose
+    cost depends on the rank, the same per-frame exchange, barrier + max-over-ranks
+    timing, one JSON line from rank 0."""
+    import torch
+    import torch.distributed as dist
+    from hpe.dist import exchange_best
+    if world > 1:
+        dist.init_process_group("gloo")
+    state = torch.zeros(27, dtype=torch.float64)
+    gathered = torch.zeros(world * 27, dtype=torch.float64)
+
+    def step(f):
+        state[:26] = float(rank)
+        state[26] = 10.0 + ((rank * 7 + f) % world)  # the winner changes from frame to frame
+        if world > 1:
+            exchange_best(state, gathered)
+
+    for f in range(args.warmup):
+        step(f)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for f in range(args.warmup, args.warmup + args.steps):
+        step(f)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": "stub exchange", "value": args.steps * world / float(t[0]),
+                          "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "stub": True,
+                          "winner_rank": int(state[0]), "winner_cost": float(state[26])}),
+              flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+# ------------------------------------------------------------------------- main
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return relaunch(args)  # before anything here touches the GPU
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with "
-                         "torch.distributed.run")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.stub:
+        stub_main(args, world, rank)
+        return 0
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -186,11 +319,9 @@ def main():
         poses = synth.trajectory(n_frames, args.seed)
         raw = [np.ascontiguousarray(ctx.render_depth(th)) for th in poses]
     sizes = [len(hpe.preprocess_depth(d, True, ds)["cloud"]) for d in raw]
-    NSLOT = 4  # frame slots in rotation: frame f+1 is prepared while frame f is tracked
-    slot = (lambda f: f) if args.resident else (lambda f: f % NSLOT)
     if args.resident:  # frames preprocessed and resident in HBM before the timed region
         for f in range(n_frames):
-            ctx.prepare_frame(slot(f), raw[f], True, ds)
+            ctx.prepare_frame(f, raw[f], True, ds)
         ctx.check(lib.hpe_sync(ctx.h))
     ub, lb, sd = hpe.reference_bounds()
     ctx.check(lib.hpe_set_pso_params(ctx.h, hpe._lib.ptr(ub, C.c_double),
@@ -206,7 +337,7 @@ def main():
 
     def step(f):
         if args.resident:
-            ctx.select_frame(slot(f))
+            ctx.select_frame(f)
             ctx.check(lib.hpe_track_frame_dev(ctx.h, P, refine, C.c_void_p(state.data_ptr())))
         else:  # frame f tracked while frame f+1 is prepared inside its refine launch
             ctx.track_pipelined(P, refine, state.data_ptr(), raw[f + 1] if f + 1 < n_frames else None)
@@ -254,8 +385,11 @@ def main():
     torch.cuda.synchronize()
     frame_us = [a.elapsed_time(b) * 1e3 for a, b in ev]
     # per-kernel durations: the same frames once more with every dispatch bracketed by
-    # hipExtLaunchKernel start/stop events (direct launches; kernels are identical)
+    # hipExtLaunchKernel start/stop events on the tracker stream the kernels run on
+    # (direct launches; kernels are identical)
     ctx.check(lib.hpe_profile_enable(ctx.h, 1))
+    rev = C.c_uint64(0)
+    ctx.check(lib.hpe_refine_eval_count(ctx.h, C.byref(rev), 1))  # reset
     if not args.resident:
         ctx.pipeline_begin(raw[args.warmup], True, ds)
     errs = []  # gnd_truth_err (costfunc.cpp:476-507) of each frame's bestp vs the true pose
@@ -273,6 +407,7 @@ def main():
         gt[:, 1:3] *= -1
         errs.append(hpe.gnd_truth_err(est, gt.ravel()))
     ctx.check(lib.hpe_sync(ctx.h))
+    ctx.check(lib.hpe_refine_eval_count(ctx.h, C.byref(rev), 1))
     prof = {}
     for name, kid in (("k_pso_gen", 0), ("k_refine", 1), ("k_pso_init", 2), ("k_pso_final", 3),
                       ("k_preprocess", 4)):
@@ -286,72 +421,74 @@ def main():
     prof["frame_graph"] = {"launches": len(frame_us), "avg_us": sum(frame_us) / len(frame_us),
                            "min_us": min(frame_us), "max_us": max(frame_us),
                            "note": "one event pair per frame, a second pass over the frames"}
+    lib_path = hpe._lib.load()._name
 
-    if rank != 0:
-        if world > 1:
-            dist.barrier()
-            dist.destroy_process_group()
-        return
-    n_pts = sizes[args.warmup]
-    evals = P * (G + 1) * args.steps * world
-    pg = prof["k_pso_gen"]
-    avg_s = pg["avg_us"] * 1e-6
-    bytes_launch = P * algorithmic_bytes_per_eval(n_pts)
-    flops_launch = P * algorithmic_flops_per_eval(n_pts)
-    achieved = bytes_launch / avg_s / 1e9 if pg["launches"] else None
-    valu = flops_launch / avg_s / 1e12 if pg["launches"] else None
-    line = {
-        "metric": "particle-evals/sec + tracked FPS, 320x240 depth, 256p x 30gen",
-        "value": evals / el,
-        "unit": "particle-evals/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": el / args.steps * 1e3,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f32+f64",
-        "data": (f"recorded: {n_frames} *_depth.bin frames from {args.frames}" if args.frames else
-                 "synthetic: seeded 26-DOF trajectory rendered from the 48-sphere model "
-                 "into 240x320 float32 mm depth (no MSRA Subject1 on the box)"),
-        "config": {"workload": ("tracked frame = " + ("" if args.resident else
-                                "next_frame preprocessing (GPU, fused into the refine launch) + ") +
-                                "refine_init_pose + pso_evolve + cal_cost(bestp)"),
-                   "particles": P, "generations": G, "maxiter": G + 1,
-                   "cloud_points": n_pts, "refine": bool(refine),
-                   "parallelism": f"subswarms x{world}, all-gather best per frame"},
-        "tracked_fps": args.steps / el,
-        "final_cost": float(final[26]),
-        "tracking_err_mm": ({"sum_wrist_tips_mean": float(np.mean(errs)),
-                             "per_joint_mean": float(np.mean(errs) / 6),
-                             "note": "gnd_truth_err (costfunc.cpp:476-507) vs the synthetic "
-                                     "trajectory's true poses, second pass over the frames"}
-                            if errs else None),
-        "roofline": {
-            "bound": "hbm", "kernel": "k_pso_gen",
-            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS if achieved else None,
-            "traffic": load_pmc(P, n_pts),
-            "avg_launch_us": pg["avg_us"], "launches": pg["launches"],
-            "bytes_per_launch": bytes_launch,
-            "flops_per_launch": flops_launch,
-            "valu_tflops": valu,
-            "valu_frac": valu / FP32_PEAK_TFLOPS if valu else None,
-            "note": "algorithmic bytes per launch = P*(24N + 2048), per-launch time from "
-                    "hipExtLaunchKernel events on the tracker stream; the generation is "
-                    "latency-bound (one particle per workgroup, 31 dependent launches per "
-                    "frame), DESIGN.md §5"},
-        "kernels": prof,
-        "host_us_per_step": host_s / args.steps * 1e6,
-    }
-    if world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args, sizes, raw if args.frames else None)
-    print(json.dumps(line), flush=True)
+    if rank == 0:
+        n_pts = sizes[args.warmup]
+        evals = P * (G + 1) * args.steps * world
+        gen = roofline_entry("k_pso_gen", prof, P, n_pts, lib_path, P)
+        ref_launches = prof["k_refine"]["launches"]
+        ref = (roofline_entry("k_refine", prof, rev.value / ref_launches, n_pts, lib_path, P)
+               if ref_launches and rev.value else None)
+        roof = dict(gen) if gen else {}
+        if roof:
+            roof["note"] = ("algorithmic bytes per launch = P x (12N + 600) (SURVEY.md §8 d2), "
+                            "per-launch time from hipExtLaunchKernel events on the tracker "
+                            "stream; the generation is latency-bound (one particle per "
+                            "workgroup, 31 dependent launches per frame), DESIGN.md §5")
+            roof["limiter"] = "latency"
+        line = {
+            "metric": "particle-evals/sec + tracked FPS, 320x240 depth, 256p x 30gen",
+            "value": evals / el,
+            "unit": "particle-evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": el / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32+f64",
+            "data": (f"recorded: {n_frames} *_depth.bin frames from {args.frames}" if args.frames
+                     else "synthetic: seeded 26-DOF trajectory rendered from the 48-sphere "
+                          "model into 240x320 float32 mm depth (no MSRA Subject1 on the box)"),
+            "config": {"workload": (f"{args.config} = {CONFIGS[args.config][2]}; step = one "
+                                    "tracked frame = " + ("" if args.resident else
+                                    "next_frame preprocessing (GPU, fused into the refine "
+                                    "launch) + ") + "refine_init_pose + pso_evolve + "
+                                    "cal_cost(bestp)"),
+                       "particles": P, "generations": G, "maxiter": G + 1,
+                       "cloud_points": n_pts, "refine": bool(refine),
+                       "parallelism": f"subswarms x{world}, all-gather best per frame"},
+            "tracked_fps": args.steps / el,
+            "final_cost": float(final[26]),
+            "tracking_err_mm": ({"sum_wrist_tips_mean": float(np.mean(errs)),
+                                 "per_joint_mean": float(np.mean(errs) / 6),
+                                 "note": "gnd_truth_err (costfunc.cpp:476-507) vs the synthetic "
+                                         "trajectory's true poses, second pass over the frames"}
+                                if errs else None),
+            "roofline": roof or None,
+            "roofline_kernels": {"k_pso_gen": gen, "k_refine": ref},
+            "refine_evals_per_frame": rev.value / max(ref_launches, 1),
+            "kernels": prof,
+            "host_us_per_step": host_s / args.steps * 1e6,
+            "lib_sha256": lib_sha256(lib_path),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            cb = cpu_baseline(args, raw if args.frames else None)
+            line["cpu_baseline"] = cb
+            line["speedup_vs_cpu"] = {"particle_evals": line["value"] / cb["value"],
+                                      "tracked_fps": line["tracked_fps"] / cb["tracked_fps"]}
+        print(json.dumps(line), flush=True)
+    hand.ctx.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    rc = main()
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(rc or 0)  # no interpreter teardown threads or children left behind

@@ -1178,7 +1178,10 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
     if (MW) mw_publish(ml, rs, MW_JOB_EXIT, 0);
     REF_TS(rs.ts_n, 7);
     if (t < HPE_DOF) x0g[t] = rs.x0[t];
-    if (t == 0 && evals_out) *evals_out = evals;
+    if (t == 0 && evals_out) {
+        *evals_out = evals;
+        atomicAdd((unsigned long long *)(evals_out + 2), (unsigned long long)evals);  // running total
+    }
 }
 
 #include "hpe_optimise.hpp"

@@ -68,6 +68,7 @@ SIGNATURES = {
     "hpe_profile_enable": (C.c_int, [C.c_void_p, C.c_int]),
     "hpe_profile_read": (C.c_int, [C.c_void_p, ip, dp, dp, dp]),
     "hpe_profile_read_kernel": (C.c_int, [C.c_void_p, C.c_int, ip, dp, dp, dp]),
+    "hpe_refine_eval_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]),
     "hpe_render_depth": (C.c_int, [C.c_void_p, dp, C.c_double, fp]),
     "hpe_debug_stamps": (C.c_int, [C.POINTER(C.c_uint64)]),
 }

@@ -208,6 +208,10 @@ int hpe_profile_read(hpe_ctx *ctx, int32_t *launches, double *total_ms, double *
                      double *max_ms);
 int hpe_profile_read_kernel(hpe_ctx *ctx, int kernel, int32_t *launches, double *total_ms,
                             double *min_ms, double *max_ms);
+/* Evaluations done by refine_init_pose launches (cal_cost2 calls, PSO.cpp:216-266) since
+ * the context was created or last reset (bench instrumentation: the algorithmic work of
+ * the k_refine launches).  Synchronises; reset != 0 zeroes the count after reading. */
+int hpe_refine_eval_count(hpe_ctx *ctx, uint64_t *total, int reset);
 
 /* Diagnostic build only (libhpe_stamps.so): per-phase shader-clock cycle sums
  * [0..31] and lap counts [32..63] of block 0, reset on read.  Returns 1 in the

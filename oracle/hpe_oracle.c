@@ -164,6 +164,37 @@ void ora_build_hand_model(const ora_hand *h, const double th[26], double S[144],
     }
 }
 
+/* gnd_truth_err, costfunc.cpp:476-507.
+ *   gndTr_joints = gnd_truth.row(frame); reshape(3, 21)       (:486-487): column-major
+ *     fill, so joint j of the reshaped matrix's column j is row elements 3j..3j+2;
+ *   hand_joints * 10.0, cols(1,2) *= -1                        (:491-492);
+ *   diff = gndTr_joints.t() - hand_joints                     (:494);
+ *   dist = sqrt(square(c0) + square(c1) + square(c2))          (:496-498), left to right;
+ *   c = sum(dist({0,4,8,12,16,20}))                            (:500-503): Armadillo's
+ *     accumulate keeps two alternating accumulators, added at the end. */
+double ora_gnd_truth_err(const double hand_joints[63], const double *gnd, int n_frames,
+                         int frame) {
+    static const int sel[6] = {0, 4, 8, 12, 16, 20};
+    double d[6];
+    for (int q = 0; q < 6; ++q) {
+        const int j = sel[q];
+        double e[3];
+        for (int c = 0; c < 3; ++c) {
+            const double g = gnd[frame + (size_t)n_frames * (size_t)(3 * j + c)];
+            double hj = hand_joints[3 * j + c] * 10.0;
+            if (c > 0) hj *= -1;
+            e[c] = g - hj;
+        }
+        d[q] = sqrt((e[0] * e[0] + e[1] * e[1]) + e[2] * e[2]);
+    }
+    double a1 = 0.0, a2 = 0.0;
+    for (int q = 0; q < 6; q += 2) {
+        a1 += d[q];
+        a2 += d[q + 1];
+    }
+    return a1 + a2;
+}
+
 /* compute_correspondences, costfunc.cpp:306-343: cv::BFMatcher(NORM_L2) on float32
  * copies.  Per OpenCV 3.0 batchDistL2_32f: dist = sqrtf(((t0*t0) + t1*t1) + t2*t2)
  * with t = q - train in float; K=1 keeps the first strictly-smaller distance,

@@ -94,6 +94,12 @@ int ora_pso_optimise(const ora_hand *h, const ora_obs *o, const double x0[26], i
                      const double stdv[26], double w, double c1, double c2, uint64_t seed,
                      double bestp[26], double *bestcost, double *gbest_trace, int nthreads);
 
+/* gnd_truth_err, costfunc.cpp:476-507: gnd is an Armadillo-layout (column-major)
+ * n_frames x 63 matrix in mm; hand_joints the 21 x 3 row-major cm joints of
+ * ora_build_hand_model (handmodel.cpp:291-296). */
+double ora_gnd_truth_err(const double hand_joints[63], const double *gnd, int n_frames,
+                         int frame);
+
 void ora_dist_transform(const double *depth_cm, float *dt_out);
 int ora_preprocess(const float *depth_mm, int to_cm, int downsample, double focal,
                    double *depth_cm_out, float *dt_out, double *cloud_out,

@@ -87,6 +87,8 @@ class Oracle:
         L.ora_pso_optimise.restype = C.c_int
         L.ora_refine_init_pose.argtypes = [C.POINTER(OraHand), C.POINTER(OraObs), dp]
         L.ora_refine_init_pose.restype = C.c_int
+        L.ora_gnd_truth_err.argtypes = [dp, dp, C.c_int, C.c_int]
+        L.ora_gnd_truth_err.restype = C.c_double
         L.ora_dist_transform.argtypes = [dp, fp]
         L.ora_preprocess.argtypes = [fp, C.c_int, C.c_int, C.c_double, dp, fp, dp, ip, dp, dp, dp]
 
@@ -190,6 +192,15 @@ class Oracle:
         x = np.array(x0, dtype=np.float64)
         ev = self.lib.ora_refine_init_pose(C.byref(h), C.byref(obs.s), _p(x, C.c_double))
         return x, ev
+
+    # ---- evaluation
+    def gnd_truth_err(self, hand_joints, gnd_truth, frame):
+        """costfunc.cpp:476-507; gnd_truth (frames, 63) in mm, handed over in Armadillo's
+        column-major layout as the reference's `mat &gnd_truth`."""
+        hj = np.ascontiguousarray(hand_joints, dtype=np.float64).reshape(63)
+        g = np.asfortranarray(np.asarray(gnd_truth, dtype=np.float64).reshape(-1, 63))
+        return self.lib.ora_gnd_truth_err(_p(hj, C.c_double), _p(g, C.c_double), g.shape[0],
+                                          int(frame))
 
     # ---- preprocessing
     def dist_transform(self, depth_cm):

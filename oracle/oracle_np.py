@@ -196,6 +196,21 @@ def collision(radii, S):
     return pen
 
 
+def gnd_truth_err(hand_joints, gnd_truth, frame):
+    """costfunc.cpp:476-507.  gnd_truth: (frames, 63) mm; .row(frame).reshape(3, 21) is a
+    column-major fill (:486-487), i.e. joint j = row[3j:3j+3]; hand_joints (21, 3) cm
+    from build_hand_model, scaled to mm with y and z negated (:491-492); the six
+    distances of wrist + finger tips {0, 4, 8, 12, 16, 20} summed by numpy here (pairwise
+    order -- the C oracle keeps Armadillo's two accumulators; they agree to an ulp)."""
+    row = np.asarray(gnd_truth, dtype=np.float64)[frame]
+    gt = row.reshape(21, 3)  # == reshape(3, 21, order='F').T
+    hj = np.asarray(hand_joints, dtype=np.float64) * 10.0
+    hj = hj * np.array([1.0, -1.0, -1.0])
+    diff = gt - hj
+    dist = np.sqrt(np.square(diff[:, 0]) + np.square(diff[:, 1]) + np.square(diff[:, 2]))
+    return float(np.sum(dist[[0, 4, 8, 12, 16, 20]]))
+
+
 class Obs:
     def __init__(self, depth_cm, dt, cloud, scale, K=None, focal=241.42):
         self.depth = depth_cm

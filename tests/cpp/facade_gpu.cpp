@@ -43,5 +43,23 @@ int main(int argc, char **argv) {
     unsigned long long s = 0;
     for (arma::uword i = 0; i < m.n_elem; ++i) s += m(i);
     std::printf("m_sum=%llu\n", s);
+    // gnd_truth_err (costfunc.cpp:476-507) of GPU-FK hand_joints: argv[3] holds a
+    // frames x 63 ground-truth matrix (mm, one frame per line), argv[4] one pose per line;
+    // the pose of line f is built and scored against row f
+    if (argc >= 5) {
+        std::ifstream gin(argv[3]), pin(argv[4]);
+        int nf = 0;
+        gin >> nf;
+        arma::mat gt(nf, 63);
+        for (int f = 0; f < nf; ++f)
+            for (int k = 0; k < 63; ++k) gin >> gt(f, k);
+        for (int f = 0; f < nf; ++f) {
+            arma::vec p(26);
+            for (int k = 0; k < 26; ++k) pin >> p(k);
+            arma::mat Sf;
+            hand.build_hand_model(p, Sf);
+            std::printf("gte%d=%.17g\n", f, cf.gnd_truth_err(gt, f));
+        }
+    }
     return 0;
 }

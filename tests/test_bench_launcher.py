@@ -1,0 +1,36 @@
+"""bench.py's multi-GPU entry on the CPU: `python bench.py --gpus 2` from a plain
+invocation re-launches itself under torch.distributed.run (one process per rank) and
+relays rank 0's JSON line; with --stub the ranks exchange stub tracker states over gloo
+through hpe.dist.exchange_best (the per-frame best-of-subswarms step, SURVEY.md §8e,
+replacing the OpenMP loop of PSO.cpp:848-861 across devices)."""
+import json
+import os
+import subprocess
+import sys
+
+import hand_data
+
+
+def _bench(*args, timeout=240):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, str(hand_data.ROOT / "bench.py"), *args],
+                         capture_output=True, text=True, timeout=timeout, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    return json.loads(lines[0])
+
+
+def test_self_launch_two_ranks_stub():
+    r = _bench("--gpus", "2", "--stub", "--steps", "3", "--warmup", "1")
+    assert r["n_gpus"] == 2 and r["steps"] == 3 and r["stub"]
+    # frame 3: rank 0 has cost 10 + 3 % 2 = 11, rank 1 10 + 10 % 2 = 10 -> rank 1 wins
+    assert r["winner_rank"] == 1 and r["winner_cost"] == 10.0
+    assert r["value"] > 0
+
+
+def test_single_rank_stub():
+    r = _bench("--stub", "--steps", "2", "--warmup", "0")
+    assert r["n_gpus"] == 1 and r["winner_rank"] == 0

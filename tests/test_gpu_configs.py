@@ -1,0 +1,167 @@
+"""GPU parity at the BASELINE.json workloads (the configs bench.py times), against the C
+oracle on the same frames, seeds and x0.
+
+  config 1  hpe_track (the C++ test_full driver) at 32 particles x maxiter 11, 10 frames
+  config 2  one frame, 256 particles x maxiter 31 (30 generations), N = 250 and N = full,
+            through pso_evolve (traces compared) and through the tracked frame
+  config 3  the 400-frame sequence, 256 x 31, refine on, temporal prior, through the
+            pipelined loop bench.py runs (hpe_track_pipelined, raw depth in)
+  config 4  one frame, 4096 particles x maxiter 41 in the auto (wave) form
+
+Tolerances (as test_gpu_parity.py): pose |diff| <= 1e-6, cost relative 1e-8, gbest /
+stagnation-count / topology traces exact (gbest relative 1e-8).  Reference:
+testmodel.cpp:104-139, PSO.cpp:717-886 (informant topology :790-812).
+"""
+import numpy as np
+import pytest
+
+import hand_data
+import oracle_np
+
+pytestmark = pytest.mark.gpu
+
+POSE_TOL, COST_RTOL = 1e-6, 1e-8
+
+
+@pytest.fixture(scope="module")
+def gh():
+    import hpe
+    return hpe.reference_hand(device=0)
+
+
+def _pso(maxiter):
+    import hpe
+    ub, lb, sd = oracle_np.reference_bounds()
+    p = hpe.PSO()
+    p.set_pso_params(ub, lb, sd, 0.7298, 1.49618, 1.49618, maxiter, 1e-8, 1e-8)
+    return p
+
+
+def _costfunc(gh, depth, downsample):
+    import hpe
+    om = hpe.observedmodel()
+    om.downsample = downsample
+    om.set_depth_mm(depth)
+    return hpe.costfunc(gh, om)
+
+
+def _check_pso(pso, cf, bestp, rb, rc, tr):
+    np.testing.assert_allclose(bestp, rb, rtol=0, atol=POSE_TOL)
+    assert abs(pso.last_gbest_cost - rc) <= COST_RTOL * abs(rc)
+    g, cnt, topo = pso.trace(cf)
+    np.testing.assert_allclose(g, tr["gbest"], rtol=COST_RTOL)
+    assert np.array_equal(cnt, tr["count"])
+    assert np.array_equal(topo, tr["topo"])
+
+
+@pytest.mark.parametrize("downsample", [True, False])
+def test_config2_single_frame_256x30(oracle, ora_hand, gh, downsample):
+    """BASELINE config 2: 256 particles x 30 generations on one frame."""
+    P, maxiter = 256, 31
+    poses = hand_data.trajectory(4, seed=2)
+    depth = gh.ctx.render_depth(poses[3])
+    obs = oracle.preprocess(depth, downsample=downsample)
+    assert (obs.n == 250) == downsample and (downsample or obs.n > 2048)
+    cf = _costfunc(gh, depth, downsample)
+    ub, lb, sd = oracle_np.reference_bounds()
+    x0 = poses[2].copy()
+    pso = _pso(maxiter)
+    bestp = np.zeros(26)
+    assert pso.pso_evolve(cf, x0, P, bestp) == 1
+    rb, rc, tr = oracle.pso_evolve(ora_hand, obs, x0, P, maxiter, lb, ub, sd, seed=1000)
+    _check_pso(pso, cf, bestp, rb, rc, tr)
+    # the same frame as a tracked frame: refine, pso_evolve, cal_cost(bestp)
+    x = x0.copy()
+    c = pso.track_frame(cf, x, P, refine=True)
+    xr, _ = oracle.refine(ora_hand, obs, x0)
+    xr, _, _ = oracle.pso_evolve(ora_hand, obs, xr, P, maxiter, lb, ub, sd, seed=1000)
+    cr = oracle.cal_cost(ora_hand, obs, xr)
+    np.testing.assert_allclose(x, xr, rtol=0, atol=POSE_TOL)
+    assert abs(c - cr) <= COST_RTOL * abs(cr)
+
+
+def test_config4_large_swarm_4096x40(oracle, ora_hand, gh):
+    """BASELINE config 4: 4096 particles x 40 generations (auto form = one wave per
+    particle; informant in-degree and inbox sizes at their largest)."""
+    P, maxiter = 4096, 41
+    poses = hand_data.trajectory(3, seed=44)
+    depth = gh.ctx.render_depth(poses[2])
+    obs = oracle.preprocess(depth)
+    cf = _costfunc(gh, depth, True)
+    ub, lb, sd = oracle_np.reference_bounds()
+    pso = _pso(maxiter)
+    bestp = np.zeros(26)
+    assert pso.pso_evolve(cf, poses[1], P, bestp) == 1
+    rb, rc, tr = oracle.pso_evolve(ora_hand, obs, poses[1], P, maxiter, lb, ub, sd, seed=1000)
+    _check_pso(pso, cf, bestp, rb, rc, tr)
+    assert tr["count"].max() >= 0 and len(tr["topo"]) == 40
+
+
+def test_config3_sequence_400_frames_pipelined(oracle, ora_hand, gh):
+    """BASELINE config 3: 400 tracked frames, 256 x 30, refine on, x0 <- previous bestp
+    (testmodel.cpp:117-139), through the pipelined loop of bench.py (raw float32 mm depth
+    in, preprocessing on the GPU inside the previous frame's refine launch).
+
+    Checked two ways: (1) every frame against the oracle started from the GPU's previous
+    pose (per-frame parity, no accumulated history); (2) the oracle running free over the
+    whole sequence, whose first divergence from the GPU (if any) is reported."""
+    import torch
+    import hpe
+    n, P, maxiter = 400, 256, 31
+    poses = hand_data.trajectory(n, seed=7)
+    raw = [np.ascontiguousarray(gh.ctx.render_depth(th)) for th in poses]
+    ctx, lib = gh.ctx, gh.ctx.lib
+    _pso(maxiter)._push(ctx)
+    state = torch.zeros(27, dtype=torch.float64, device="cuda:0")
+    state[:26] = torch.from_numpy(poses[0].copy())
+    torch.cuda.synchronize()
+    ctx.pipeline_begin(raw[0], True, True)
+    gx, gc = [], []
+    for f in range(n):
+        ctx.track_pipelined(P, 1, state.data_ptr(), raw[f + 1] if f + 1 < n else None)
+        ctx.check(lib.hpe_sync(ctx.h))
+        torch.cuda.synchronize()
+        s = state.cpu().numpy()
+        gx.append(s[:26].copy())
+        gc.append(s[26])
+    gx, gc = np.array(gx), np.array(gc)
+    ub, lb, sd = oracle_np.reference_bounds()
+    free = poses[0].copy()
+    first_div = None
+    for f in range(n):
+        obs = oracle.preprocess(raw[f])
+        x0 = poses[0] if f == 0 else gx[f - 1]
+        xr, _ = oracle.refine(ora_hand, obs, x0)
+        xr, _, _ = oracle.pso_evolve(ora_hand, obs, xr, P, maxiter, lb, ub, sd, seed=1000)
+        cr = oracle.cal_cost(ora_hand, obs, xr)
+        assert np.abs(gx[f] - xr).max() <= POSE_TOL, f"frame {f}: pose {np.abs(gx[f] - xr).max()}"
+        assert abs(gc[f] - cr) <= COST_RTOL * abs(cr), f"frame {f}: cost {gc[f]} vs {cr}"
+        if first_div is None:
+            free, _ = oracle.refine(ora_hand, obs, free)
+            free, _, _ = oracle.pso_evolve(ora_hand, obs, free, P, maxiter, lb, ub, sd, seed=1000)
+            if np.abs(free - gx[f]).max() > POSE_TOL:
+                first_div = f
+    print(f"400-frame sequence: per-frame parity on all frames; free-running oracle first "
+          f"diverges at frame {first_div}")
+    assert first_div is None, f"free-running oracle diverges from the GPU at frame {first_div}"
+
+
+def test_config1_hpe_track_32x10(tmp_path, oracle, ora_hand, np_hand):
+    """BASELINE config 1's shape (32 particles x maxiter 11) through the C++ test_full
+    driver over 10 .bin frames, against the oracle loop."""
+    from test_gpu_facade import _run_track, _write_inputs
+    n, P, maxiter = 10, 32, 11
+    poses = hand_data.trajectory(n, seed=13)
+    hand, frames, depth = _write_inputs(tmp_path, np_hand, poses)
+    ub, lb, sd = oracle_np.reference_bounds()
+    x = oracle_np.X0.copy()
+    ref_c, ref_x = [], []
+    for f in range(n):
+        obs = oracle.preprocess(depth[f])
+        x, _ = oracle.refine(ora_hand, obs, x)
+        x, _, _ = oracle.pso_evolve(ora_hand, obs, x, P, maxiter, lb, ub, sd)
+        ref_c.append(oracle.cal_cost(ora_hand, obs, x))
+        ref_x.append(x.copy())
+    c, xs = _run_track(hand, frames, n, P, maxiter, 1, tmp_path / "poses.txt")
+    np.testing.assert_allclose(xs, np.array(ref_x), rtol=0, atol=POSE_TOL)
+    np.testing.assert_allclose(c, np.array(ref_c), rtol=COST_RTOL, atol=0)

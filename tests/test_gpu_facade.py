@@ -124,3 +124,48 @@ def test_term_api_matches_oracle(oracle, ora_hand, np_hand):
         np.testing.assert_array_equal(Sd[:, 1:], -S[:, 1:])  # un-negated like :249
         np.testing.assert_allclose(cf.self_collision_penalty(S, gh.get_radii()), tr[2],
                                    rtol=1e-9, atol=1e-300)
+
+
+def test_gnd_truth_err_gpu_joints(tmp_path, oracle, ora_hand, np_hand):
+    """costfunc::gnd_truth_err (costfunc.cpp:476-507, SURVEY.md §8 f4) on joints built by
+    the GPU FK (hpe_build_spheres joints_out), through the Python mirror and through the
+    C++ façade (arma mat, column-major, reshape(3,21) fill, y/z flip), against the C
+    oracle on its own FK joints.  Tolerance: the joints agree to 1e-9 cm (fp64 FK, only
+    sin/cos rounding differs), so the mm error sums agree to 1e-7 mm absolute."""
+    import hpe
+    from test_oracle_kat import _gt_matrix
+    rng = np.random.default_rng(41)
+    poses = hand_data.trajectory(6, seed=41)
+    gt = _gt_matrix(oracle, ora_hand, poses, rng)
+    est = poses[::-1].copy()  # score pose 5-f against ground-truth row f
+    gh = hpe.reference_hand(0)
+    om = hpe.observedmodel(); om.downsample = True
+    om.set_depth_mm(oracle_np.render_depth_mm(np_hand, poses[0]))
+    cf = hpe.costfunc(gh, om)
+    ref, mirror = [], []
+    for f, th in enumerate(est):
+        _, J = oracle.build(ora_hand, th, joints=True)
+        ref.append(oracle.gnd_truth_err(J, gt, f))
+        gh.build_hand_model(th)  # GPU FK -> hand_joints
+        np.testing.assert_allclose(gh.hand_joints, J, rtol=0, atol=1e-9)
+        mirror.append(cf.gnd_truth_err(gt, f))
+    np.testing.assert_allclose(mirror, ref, rtol=0, atol=1e-7)
+    # the C++ façade on the same inputs
+    src = hand_data.ROOT / "tests" / "cpp" / "facade_gpu.cpp"
+    exe = tmp_path / "facade_gpu"
+    subprocess.run(["g++", "-O1", "-std=c++17", "-o", str(exe), str(src),
+                    f"-I{PKG / 'facade'}", f"-L{PKG}", "-lhpe_facade", "-lhpe",
+                    f"-Wl,-rpath,{PKG}"], check=True, timeout=120)
+    hand, frames, _ = _write_inputs(tmp_path, np_hand, poses[:1])
+    gtf, pf = tmp_path / "gt.txt", tmp_path / "poses.txt"
+    with open(gtf, "w") as fh:
+        fh.write(f"{len(gt)}\n")
+        np.savetxt(fh, gt, fmt="%.17g")
+    np.savetxt(pf, est, fmt="%.17g")
+    out = subprocess.run([str(exe), str(hand), str(frames) + "/", str(gtf), str(pf)],
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    vals = dict(l.split("=", 1) for l in out.stdout.split() if "=" in l)
+    fac = [float(vals[f"gte{f}"]) for f in range(len(est))]
+    np.testing.assert_allclose(fac, ref, rtol=0, atol=1e-7)
+    assert fac == mirror  # same joints, same operation order

@@ -217,3 +217,44 @@ def test_check_constraints_quirk_via_pso(oracle, ora_hand):
     ub2[6:] = 1e-3
     bp, bc, tr = oracle.pso_evolve(ora_hand, obs, oracle_np.X0, 8, 4, lb2, ub2, sd)
     assert np.all(bp[6:] >= lb2[6:])
+
+
+def _gt_matrix(oracle, ora_hand, poses, rng, noise_mm=4.0):
+    """A frames x 63 ground-truth matrix in the MSRA layout costfunc.cpp:476-507 reads:
+    row f = the 21 joints of poses[f] in mm, joint j at columns 3j..3j+2, with y and z
+    negated (the reference flips its model joints to compare, :492), plus noise."""
+    rows = []
+    for th in poses:
+        _, J = oracle.build(ora_hand, th, joints=True)
+        g = J * 10.0
+        g[:, 1:3] *= -1
+        rows.append((g + rng.normal(scale=noise_mm, size=g.shape)).ravel())
+    return np.array(rows)
+
+
+def test_gnd_truth_err_oracles(oracle, ora_hand, np_hand):
+    """costfunc.cpp:476-507: the C oracle (Armadillo's column-major
+    matrix, reshape(3,21) fill, two-accumulator sum), the numpy restatement and the
+    product's host mirror agree; zero at the true pose; a known six-joint offset."""
+    import hpe
+    rng = np.random.default_rng(12)
+    poses = hand_data.trajectory(5, seed=12)
+    gt = _gt_matrix(oracle, ora_hand, poses, rng)
+    for f, th in enumerate(poses[::-1]):  # estimate = a different pose of the sequence
+        _, J = oracle.build(ora_hand, th, joints=True)
+        Jn = np_hand.build_hand_model(th, return_joints=True)[1]
+        np.testing.assert_allclose(Jn, J, rtol=0, atol=1e-12)
+        ref = oracle.gnd_truth_err(J, gt, f)
+        assert ref > 0
+        assert abs(oracle_np.gnd_truth_err(J, gt, f) - ref) <= 4 * np.spacing(ref)
+        assert hpe.gnd_truth_err(J, gt[f]) == ref  # same operation order: bit-identical
+    _, J = oracle.build(ora_hand, poses[2], joints=True)
+    exact = _gt_matrix(oracle, ora_hand, poses, rng, noise_mm=0.0)
+    assert oracle.gnd_truth_err(J, exact, 2) == 0.0
+    shifted = exact.copy()
+    shifted[2, [3 * j + 1 for j in (0, 4, 8, 12, 16, 20)]] += 2.5  # 2.5 mm along y
+    assert abs(oracle.gnd_truth_err(J, shifted, 2) - 15.0) < 1e-12
+    # only the wrist and the five tips count: moving joint 1 changes nothing
+    other = exact.copy()
+    other[2, 3:6] += 100.0
+    assert oracle.gnd_truth_err(J, other, 2) == 0.0

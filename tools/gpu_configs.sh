@@ -1,10 +1,12 @@
-# BASELINE configs on one GPU: default e2e bench (with CPU baseline),
-# N = full cloud, the 400-frame sequence (config 3), 4096 x 40 (config 4).
+# BASELINE configs on one GPU, each its own bench.py run: N = full
+# cloud, the 400-frame sequence (config 3), 4096 x 40 (config 4), 32 x 10 (config 1's
+# shape), one 1024-particle subswarm of config 5, the resident-frames variant.
 set -o pipefail
-O=gpurun_out/configs
+O=gpurun_out/${1:-r02}/configs
 rm -rf $O; mkdir -p $O
-timeout -k 10 300 python bench.py > $O/default.log 2>&1 && \
 timeout -k 10 300 python bench.py --full-cloud --no-cpu-baseline > $O/full_cloud.log 2>&1 && \
 timeout -k 10 300 python bench.py --steps 400 --warmup 1 --no-cpu-baseline > $O/seq400.log 2>&1 && \
-timeout -k 10 300 python bench.py --particles 4096 --generations 40 --no-cpu-baseline > $O/p4096.log 2>&1 && \
-timeout -k 10 300 python bench.py --particles 32 --generations 10 --no-cpu-baseline > $O/p32.log 2>&1
+timeout -k 10 300 python bench.py --config p4096 --no-cpu-baseline > $O/p4096.log 2>&1 && \
+timeout -k 10 300 python bench.py --config p32 --no-cpu-baseline > $O/p32.log 2>&1 && \
+timeout -k 10 300 python bench.py --config subswarm8 --no-cpu-baseline > $O/subswarm1.log 2>&1 && \
+timeout -k 10 300 python bench.py --resident --no-cpu-baseline > $O/resident.log 2>&1

@@ -12,11 +12,13 @@ usage: prof_summary.py stats RUN_DIR OUT.csv
 """
 import csv
 import glob
+import hashlib
 import json
 import os
 import sqlite3
 import sys
 from collections import defaultdict
+from pathlib import Path
 
 
 def _db(d):
@@ -72,7 +74,10 @@ def pmc(fetch_dir, write_dir, kernel, P, N, out):
     f = [v for n, v in counter_rows(fetch_dir, "FETCH_SIZE") if short(n) == kernel]
     w = [v for n, v in counter_rows(write_dir, "WRITE_SIZE") if short(n) == kernel]
     fk, wk = sum(f) / len(f), sum(w) / len(w)
+    lib = Path(__file__).resolve().parent.parent / "hand-pose-estimation_amd" / \
+        os.environ.get("HPE_LIB_VARIANT", "libhpe.so")
     res = {"kernel": kernel, "particles": P, "cloud_points": N,
+           "lib_sha256": hashlib.sha256(lib.read_bytes()).hexdigest(),
            "dispatches": {"fetch_pass": len(f), "write_pass": len(w)},
            "fetch_size_kb_raw": fk, "write_size_kb": wk,
            "bytes_per_launch": (2 * fk + wk) * 1024,
