@@ -12,13 +12,16 @@ import numpy as np
 from . import X0, Context, preprocess_depth, reference_bounds
 
 
-def trajectory(n_frames: int, seed: int = 0, step: float = 0.15) -> np.ndarray:
+def trajectory(n_frames: int, seed: int = 0, step: float = 0.15,
+               revert: float = 0.0) -> np.ndarray:
+    """revert > 0 pulls the pose back towards x0 (long sequences stay in view)."""
     rng = np.random.default_rng(seed)
     ub, lb, sd = reference_bounds()
     poses = [X0.copy()]
     vel = np.zeros(26)
     for _ in range(n_frames - 1):
         vel = 0.8 * vel + 0.2 * rng.standard_normal(26) * sd * step
+        vel += revert * (X0 - poses[-1])
         poses.append(np.clip(poses[-1] + vel, lb, ub))
     return np.array(poses)
 

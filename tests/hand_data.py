@@ -22,8 +22,9 @@ def random_thetas(rng, P, x0=None, spread=1.0):
     return np.clip(th, lb, ub)
 
 
-def trajectory(n_frames, seed=0):
-    """Smooth seeded pose sequence starting at testmodel.cpp's x0."""
+def trajectory(n_frames, seed=0, revert=0.0):
+    """Smooth seeded pose sequence starting at testmodel.cpp's x0 (SURVEY.md §8 d1);
+    revert > 0 pulls the pose back towards x0 so that long sequences stay in view."""
     import oracle_np
     rng = np.random.default_rng(seed)
     ub, lb, sd = oracle_np.reference_bounds()
@@ -31,5 +32,6 @@ def trajectory(n_frames, seed=0):
     vel = np.zeros(26)
     for _ in range(n_frames - 1):
         vel = 0.8 * vel + 0.2 * rng.standard_normal(26) * sd * 0.15
+        vel += revert * (oracle_np.X0 - poses[-1])
         poses.append(np.clip(poses[-1] + vel, lb, ub))
     return np.array(poses)
