@@ -71,8 +71,9 @@ def stats(run_dir, out):
 
 
 def pmc(fetch_dir, write_dir, kernel, P, N, out):
-    f = [v for n, v in counter_rows(fetch_dir, "FETCH_SIZE") if short(n) == kernel]
-    w = [v for n, v in counter_rows(write_dir, "WRITE_SIZE") if short(n) == kernel]
+    match = lambda n: short(n) == kernel or short(n).startswith(kernel + "<")  # noqa: E731
+    f = [v for n, v in counter_rows(fetch_dir, "FETCH_SIZE") if match(n)]
+    w = [v for n, v in counter_rows(write_dir, "WRITE_SIZE") if match(n)]
     fk, wk = sum(f) / len(f), sum(w) / len(w)
     lib = Path(__file__).resolve().parent.parent / "hand-pose-estimation_amd" / \
         os.environ.get("HPE_LIB_VARIANT", "libhpe.so")
