@@ -410,7 +410,7 @@ def main():
     ctx.check(lib.hpe_refine_eval_count(ctx.h, C.byref(rev), 1))
     prof = {}
     for name, kid in (("k_pso_gen", 0), ("k_refine", 1), ("k_pso_init", 2), ("k_pso_final", 3),
-                      ("k_preprocess", 4)):
+                      ("k_preprocess", 4), ("k_pso_loop", 7)):
         nl = C.c_int32(0); tot = C.c_double(0); mn = C.c_double(0); mx = C.c_double(0)
         ctx.check(lib.hpe_profile_read_kernel(ctx.h, kid, C.byref(nl), C.byref(tot),
                                               C.byref(mn), C.byref(mx)))
@@ -426,16 +426,26 @@ def main():
     if rank == 0:
         n_pts = sizes[args.warmup]
         evals = P * (G + 1) * args.steps * world
+        # the PSO generations: one k_pso_loop launch per frame (G generations, grid-resident
+        # form) or one k_pso_gen launch per generation
+        loop = roofline_entry("k_pso_loop", prof, P * G, n_pts, lib_path, P)
         gen = roofline_entry("k_pso_gen", prof, P, n_pts, lib_path, P)
         ref_launches = prof["k_refine"]["launches"]
         ref = (roofline_entry("k_refine", prof, rev.value / ref_launches, n_pts, lib_path, P)
                if ref_launches and rev.value else None)
-        roof = dict(gen) if gen else {}
+        roof = dict(loop or gen or {})
         if roof:
-            roof["note"] = ("algorithmic bytes per launch = P x (12N + 600) (SURVEY.md §8 d2), "
-                            "per-launch time from hipExtLaunchKernel events on the tracker "
-                            "stream; the generation is latency-bound (one particle per "
-                            "workgroup, 31 dependent launches per frame), DESIGN.md §5")
+            if loop:
+                roof["us_per_generation"] = loop["avg_launch_us"] / G
+            roof["note"] = ("algorithmic bytes per launch = evaluations per launch x (12N + 600) "
+                            "(SURVEY.md §8 d2), per-launch time from hipExtLaunchKernel events on "
+                            "the tracker stream; " + (
+                                f"k_pso_loop = the {G} generations of a frame in one grid-"
+                                "resident launch (one workgroup per particle, generations "
+                                "separated by data-tagged granule waits)" if loop else
+                                "k_pso_gen = one generation per launch") +
+                            "; latency-bound (one particle per workgroup, dependent "
+                            "generations), DESIGN.md §5")
             roof["limiter"] = "latency"
         line = {
             "metric": "particle-evals/sec + tracked FPS, 320x240 depth, 256p x 30gen",
@@ -468,7 +478,7 @@ def main():
                                          "trajectory's true poses, second pass over the frames"}
                                 if errs else None),
             "roofline": roof or None,
-            "roofline_kernels": {"k_pso_gen": gen, "k_refine": ref},
+            "roofline_kernels": {"k_pso_loop": loop, "k_pso_gen": gen, "k_refine": ref},
             "refine_evals_per_frame": rev.value / max(ref_launches, 1),
             "kernels": prof,
             "host_us_per_step": host_s / args.steps * 1e6,

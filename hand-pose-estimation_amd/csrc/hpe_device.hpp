@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "hpe_layout.hpp"
 
 // Diagnostic phase stamps (libhpe_stamps.so only, -DHPE_STAMPS=1; the product build
@@ -199,7 +201,18 @@ struct FkX {
     double x[15][5];
 };
 
-template <int MODE>
+// ocml's fp64 sincos as an out-of-line call: inside a persistent loop (k_pso_loop) the
+// inlined version's ~20 polynomial constants are hoisted out of the loop and spilled.
+struct SinCos {
+    double s, c;
+};
+__device__ __noinline__ SinCos sincos_outline(double a) {
+    SinCos r;
+    sincos(a, &r.s, &r.c);
+    return r;
+}
+
+template <int MODE, bool OUTLINE_TRIG = false>
 __device__ __forceinline__ void fk_wave_t(FkSm &f, const DevHand *__restrict__ H, FkX *X) {
     const int l = threadIdx.x & 63;
     StampClock sc;
@@ -228,7 +241,13 @@ __device__ __forceinline__ void fk_wave_t(FkSm &f, const DevHand *__restrict__ H
             else if (l < 3) a = deg2rad(f.th[l]);    // ANG, ROT
             else a = deg2rad(f.th[6 + (l - 3)]);     // digit angles, handmodel.cpp:141-146
             double s, c;
-            sincos(a, &s, &c);
+            if (OUTLINE_TRIG) {
+                const SinCos r = sincos_outline(a);
+                s = r.s;
+                c = r.c;
+            } else {
+                sincos(a, &s, &c);
+            }
             f.sn[l] = s;
             f.cs[l] = c;
         }
@@ -324,8 +343,9 @@ __device__ __forceinline__ void fk_wave_t(FkSm &f, const DevHand *__restrict__ H
     sc.lap(14);
 }
 
+template <bool OUTLINE_TRIG = false>
 __device__ __forceinline__ void fk_wave(FkSm &f, const DevHand *__restrict__ H) {
-    fk_wave_t<FK_FULL>(f, H, nullptr);
+    fk_wave_t<FK_FULL, OUTLINE_TRIG>(f, H, nullptr);
 }
 
 // ---------------------------------------------------------------- reductions
@@ -566,9 +586,8 @@ __device__ __forceinline__ double search_align(const FkSm &f, const CV &cv,
     typedef float f2 __attribute__((ext_vector_type(2)));  // packed fp32 (v_pk_*_f32)
     const float *SX = f.Sp[0] + 24 * h, *SY = f.Sp[1] + 24 * h, *SZ = f.Sp[2] + 24 * h;
     BLK_TS(g_ts, 15);
-    for (int it = gt; it < 2 * cv.n; it += NT) {
+    auto item = [&](int it, const Pt &q) {
         const int p = it >> 1;
-        const Pt q = (it == gt) ? pre : load_pt(cv, it);
         const double X = q.x, Y = q.y, Z = q.z;
         const float qx = (float)X, qy = (float)Y, qz = (float)Z;
         float d2[24];
@@ -638,6 +657,21 @@ __device__ __forceinline__ double search_align(const FkSm &f, const CV &cv,
         }
         if (HPE_STAMPS) asm volatile("" ::"v"(acc));
         BLK_TS(g_ts, 14);
+    };
+    if (std::is_same<CV, CloudGlobal>::value && 2 * cv.n > NT) {
+        // Several items per lane from HBM (full cloud, wave form): the next item's point
+        // is loaded one item ahead (unconditionally, at a clamped index), so its L2 round
+        // trip overlaps this item's search instead of opening every iteration.  (An LDS
+        // cloud, refine and pso_optimise, keeps the plain loop: no register cost.)
+        Pt q = pre;
+        for (int it = gt; it < 2 * cv.n; it += NT) {
+            const int pn = min((it + NT) >> 1, cv.n - 1);
+            const Pt qn = Pt{cv.cx[pn], cv.cy[pn], cv.cz[pn]};
+            item(it, q);
+            q = qn;
+        }
+    } else {
+        for (int it = gt; it < 2 * cv.n; it += NT) item(it, it == gt ? pre : load_pt(cv, it));
     }
     return acc;
 }
