@@ -637,23 +637,38 @@ __device__ __forceinline__ double search_align(const FkSm &f, const CV &cv,
         // 5 ulps of the nearest, ahead of it: rare) is the exact class needed, by the whole
         // wave.  The check recomputes that sphere's fp32 d2 with the search's operations.
         int idx = first_le(__float_as_int(m) + 5);
+        // the candidate's fp64 centre and radius, read ONCE: the exact check uses the float
+        // of the centre (= Sp) and, unless the rare exact-class path moves idx, the
+        // alignment uses them as they are (one LDS round trip on the chain, not two)
+        int ic = idx < HPE_NS ? idx : 0;  // >= 48: all-NaN point (reference undefined)
+        double cx = 0, cy = 0, cz = 0, cr = 0;
         bool exact = true;
         if (h == 0) {
-            const int ic = idx < HPE_NS ? idx : 0;
-            const float tx = qx - (float)f.S[ic][0], ty = qy - (float)f.S[ic][1],
-                        tz = qz - (float)f.S[ic][2];
+            cx = f.S[ic][0];
+            cy = f.S[ic][1];
+            cz = f.S[ic][2];
+            cr = H->radii[ic];
+            const float tx = qx - (float)cx, ty = qy - (float)cy, tz = qz - (float)cz;
             const float dc = (tx * tx + ty * ty) + tz * tz;
             exact = (dc == m);  // false for NaN
         }
-        if (__ballot(!exact)) idx = first_le(__float_as_int(hi_sqrt_class(m)));
+        if (__ballot(!exact)) {
+            idx = first_le(__float_as_int(hi_sqrt_class(m)));
+            ic = idx < HPE_NS ? idx : 0;
+            if (h == 0) {
+                cx = f.S[ic][0];
+                cy = f.S[ic][1];
+                cz = f.S[ic][2];
+                cr = H->radii[ic];
+            }
+        }
         if (HPE_STAMPS) asm volatile("" ::"v"(idx));
         BLK_TS(g_ts, 13);
         if (h == 0) {
-            if (idx >= HPE_NS) idx = 0;  // all-NaN point: reference is undefined (trainIdx -1)
-            const double dx = X - f.S[idx][0], dy = Y - f.S[idx][1], dz = Z - f.S[idx][2];
-            const double e = sqrt((dx * dx + dy * dy) + dz * dz) - H->radii[idx];
+            const double dx = X - cx, dy = Y - cy, dz = Z - cz;
+            const double e = sqrt((dx * dx + dy * dy) + dz * dz) - cr;
             acc += e * e;
-            if (STORE_MATCH) match[p] = idx;
+            if (STORE_MATCH) match[p] = ic;
         }
         if (HPE_STAMPS) asm volatile("" ::"v"(acc));
         BLK_TS(g_ts, 14);
