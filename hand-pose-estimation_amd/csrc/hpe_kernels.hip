@@ -756,6 +756,27 @@ __device__ __forceinline__ void push_lane_links(const DevSwarm &sw, int g, int i
     }
 }
 
+// The wave form's pushes: {tag, cost} as ONE 16-B entry of the compact array ibtc
+// [g&1][var][receiver][slot] (the receiver reads its K entries of a variant as one
+// contiguous run, 2 lines, instead of the first 16 B of K rows, K lines), the pbest row into
+// fields 2..27 of the inbox row (read only for the chosen informant).
+__device__ __forceinline__ size_t ibtc_index(const DevSwarm &sw, int par, int var, int r, int slot) {
+    return (((size_t)par * 2 + var) * sw.P + r) * sw.K + slot;
+}
+__device__ __forceinline__ void push_inbox_w(const DevSwarm &sw, int g, int s, int q, const Link &L,
+                                             int tt, double pc, const double *row) {
+    const int r = L.ok ? (int)(L.raw & 0xffffffff) : -1, slot = (int)(L.raw >> 32);
+    if (r < 0) return;
+    const int dst = q / IB_FIELDS, fld = q - IB_FIELDS * dst, var = dst < 3 ? 1 : 0;
+    if (fld == 0) {
+        typedef double d2v __attribute__((ext_vector_type(2)));
+        const d2v e = {__longlong_as_double(((long long)g << 48) | ((long long)tt << 32) | s), pc};
+        *(d2v *)(sw.ibtc + 2 * ibtc_index(sw, g & 1, var, r, slot)) = e;
+    } else if (fld >= 2) {
+        sw.inbox[ib_index(sw, g & 1, var, r, slot) + fld] = row[fld - 2];
+    }
+}
+
 __global__ __launch_bounds__(PW_NT) void k_pso_init_w(DevSwarm sw, const double *__restrict__ x0,
                                                       const DevObs *__restrict__ og,
                                                       const DevHand *__restrict__ Hg) {
@@ -793,7 +814,7 @@ __global__ __launch_bounds__(PW_NT) void k_pso_init_w(DevSwarm sw, const double 
         gmin_lower(sw, 0, i, c);
     }
 #pragma unroll
-    for (int k = 0; k < 3; ++k) push_inbox(sw, 0, i, l + 64 * k, lk[k], 1, c, f.th);
+    for (int k = 0; k < 3; ++k) push_inbox_w(sw, 0, i, l + 64 * k, lk[k], 1, c, f.th);
 }
 
 __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *__restrict__ og,
@@ -824,10 +845,11 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
     const double pci = sw.pch[(size_t)(g - 1) * P + ic];
     double tg[2], tc[2];
 #pragma unroll
-    for (int vr = 0; vr < 2; ++vr) {
-        const double *sl = sw.inbox + ib_index(sw, (g - 1) & 1, vr, ic, l < K ? l : K - 1);
-        tg[vr] = sl[0];
-        tc[vr] = sl[1];
+    for (int vr = 0; vr < 2; ++vr) {  // {tag, cost} of slot l: one 16-B load, contiguous run
+        typedef double d2v __attribute__((ext_vector_type(2)));
+        const d2v e = *(const d2v *)(sw.ibtc + 2 * ibtc_index(sw, (g - 1) & 1, vr, ic, l < K ? l : K - 1));
+        tg[vr] = e.x;
+        tc[vr] = e.y;
     }
     const unsigned long long gcell = gmin_load(sw, g - 1);
     const Sig pv = sw.sig[g > 1 ? g - 1 : 0];
@@ -914,7 +936,7 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const int q = l + 64 * k;
-        push_inbox(sw, g, i, q, lk[k], q < 3 * IB_FIELDS ? g + 1 : topo, pn, f.th);
+        push_inbox_w(sw, g, i, q, lk[k], q < 3 * IB_FIELDS ? g + 1 : topo, pn, f.th);
     }
 }
 

@@ -64,6 +64,7 @@ struct DevSwarm {
     double *pb;               // P x 26           pbest positions (own particle only)
     double *v;                // P x 26           velocities (own particle only)
     double *inbox;            // 2 x 2 x P x K x IB_FIELDS  [g&1][kept, rebuilt][receiver][slot]
+    double *ibtc;             // 2 x 2 x P x K x {tag, cost}  (wave form: compact informant costs)
     unsigned long long *gmin; // (G+1) x GMIN_SHARDS cells (128-B apart): min pbest cost bits
                               // per generation, particle i lowering shard i % GMIN_SHARDS
     Sig *sig;                 // G+1              gbest cost / count / topology per generation
