@@ -967,15 +967,22 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
     // a k_pso_loop wait timed out (sw.err): the result is reported as a NaN cost
     const bool aborted = sw.err && *sw.err != 0;
     if (t == 0 && sw.epoch) atomicAdd(sw.epoch, 1u);  // the next call's granule tags
-    if (TAIL && seq_dev && t == 0) {
+    if (TAIL && seq_dev && t == HPE_NT - 64) {
         // pipelined tracking: this frame's refine launch (and the preparation of the next
         // frame inside it, which read a pinned host buffer) has completed; publish the
-        // frame's sequence number to the host, which polls it before reusing that buffer
+        // frame's sequence number to the host, which polls it before reusing that buffer.
+        // Relaxed: the kernel boundary already retired those reads, and no store of this
+        // kernel needs publishing with it.  Wave 7, idle until the first barrier, takes the
+        // counter's load round trip instead of wave 0, which reads the gmin history.
         const unsigned long long n = *seq_dev + 1;
         *seq_dev = n;
-        __hip_atomic_store(done_host, n, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(done_host, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if (TAIL) stage_hand<HPE_NT>(sm.hand, Hg);
+    // the frame descriptor handed back at the end, loaded now (off the final chain)
+    const unsigned long long obs_word =
+        (TAIL && obs_out && t < (int)(sizeof(DevObs) / 8)) ? ((const unsigned long long *)og)[t] : 0ull;
+    double bp = 0.0;  // gbest_pos = zeros<vec> (PSO.cpp:739) if nothing beat 1e100
     double gcost = 1e100;
     int last = -1, count = 100;
     for (int base = 0; base <= G; base += CH) {
@@ -1034,20 +1041,20 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
             }
         }
         const VI b = block_argmin(sm, mine);
-        if (t < HPE_DOF) out[t] = sw.xh[((size_t)last * P + b.i) * HPE_DOF + t];
-    } else if (t < HPE_DOF) {
-        out[t] = 0.0;  // gbest_pos = zeros<vec> (PSO.cpp:739) if nothing beat 1e100
+        if (t < HPE_DOF) bp = sw.xh[((size_t)last * P + b.i) * HPE_DOF + t];
+    }
+    // bestp stays in each thread's register: no barrier and no re-read of `out`
+    if (t < HPE_DOF) {
+        out[t] = bp;
+        sw.gpos[t] = bp;
     }
     if (t == 0) out[HPE_DOF] = aborted ? __builtin_nan("") : gcost;
-    __syncthreads();
-    if (t < HPE_DOF) sw.gpos[t] = out[t];
     for (int c = t; c < (G + 1) * GMIN_SHARDS; c += HPE_NT) sw.gmin[(size_t)c * GMIN_STRIDE] = ~0ull;
     if (TAIL) {
-        if (obs_out && t < (int)(sizeof(DevObs) / 8))
-            ((unsigned long long *)obs_out)[t] = ((const unsigned long long *)og)[t];
+        if (obs_out && t < (int)(sizeof(DevObs) / 8)) ((unsigned long long *)obs_out)[t] = obs_word;
         if (same_eval && last >= 0) return;  // out[26] = gcost = cal_cost(bestp)
         const DevObs o = *og;
-        if (t < HPE_DOF) sm.fk.th[t] = out[t];
+        if (t < HPE_DOF) sm.fk.th[t] = bp;
         const CloudGlobal cv = obs_cloud(o);
         const Pt pre = load_pt(cv, t);
         __syncthreads();
