@@ -725,6 +725,9 @@ __device__ __forceinline__ double align_frozen(const FkSm &f, const CV &cv,
     return (a0 + a1) + (a2 + a3);
 }
 
+#ifndef HPE_SETPRIO_FROM
+#define HPE_SETPRIO_FROM 4  // first wave of a 512-thread block raised during the search
+#endif
 enum EvalMode { EV_COST = 0, EV_COST2_CORR = 1, EV_COST2_FROZEN = 2, EV_COST_STORE = 3 };
 
 // cal_cost of the particle in f.th by ONE wave (FK + search over 64 lanes): the
@@ -766,11 +769,17 @@ __device__ __forceinline__ double eval_block(Smem &sm, const DevObs &o, const CV
     const int t = threadIdx.x;
     // issue the depth gathers first: their latency hides under the search
     const DepthG dg = depth_issue_w0(sm.fk, o, H);
+    // Waves 4..7 share the SIMDs with waves 0..3 and lose the age arbitration: they reached
+    // the reduction ~0.5 us after waves 1..3.  Static priority for that half during the
+    // search (MI355X_MICROARCH.md, two waves per SIMD, item 4).
+    const bool young = NT == 512 && (t >> 6) >= HPE_SETPRIO_FROM;
+    if (young) __builtin_amdgcn_s_setprio(1);
     double al;
     if (MODE == EV_COST2_FROZEN) al = align_frozen(sm.fk, cv, H, match, t, NT);
     else if (MODE == EV_COST2_CORR || MODE == EV_COST_STORE)
         al = search_align<NT, true>(sm.fk, cv, H, match, pre);
     else al = search_align<NT, false>(sm.fk, cv, H, nullptr, pre, -1, g_ts);
+    if (young) __builtin_amdgcn_s_setprio(0);
     const bool coll = (MODE == EV_COST2_CORR || MODE == EV_COST2_FROZEN);
     double co = (coll && t < 144) ? collide_term(sm.fk, t, H) : 0.0;
     BLK_TS(g_ts, 8);

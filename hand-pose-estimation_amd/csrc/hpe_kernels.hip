@@ -1220,7 +1220,10 @@ __device__ __forceinline__ double eval_corr(RefineSm &rs, const DevObs &o, const
     const int t = threadIdx.x;
     if (MW) mw_publish(*ml, rs, MW_JOB_CORR, 1);
     const DepthG dg = depth_issue_w0(rs.base, o, H);
+    const bool young = (t >> 6) >= HPE_SETPRIO_FROM;  // as in eval_block
+    if (young) __builtin_amdgcn_s_setprio(1);
     double al = MW ? 0.0 : search_align<RF_NT, true>(rs.base, cv, H, match, load_pt(cv, t));
+    if (young) __builtin_amdgcn_s_setprio(0);
     double co = (t < 144) ? collide_term(rs.base, t, H) : 0.0;
     double dep = depth_finish(dg, o, t < HPE_NS);
     block_sum3<RF_NT>(rs.red, al, dep, co);  // also publishes matchId to the block
