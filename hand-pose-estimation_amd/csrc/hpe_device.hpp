@@ -236,10 +236,11 @@ __device__ __forceinline__ void fk_wave_t(FkSm &f, const DevHand *__restrict__ H
     }
     if (MODE != FK_TRANSLATE) {
         if (l < 23) {
-            double a;
-            if (l == 0) a = deg2rad(f.th[0] + 180);  // TWS, fingermodel.cpp:91
-            else if (l < 3) a = deg2rad(f.th[l]);    // ANG, ROT
-            else a = deg2rad(f.th[6 + (l - 3)]);     // digit angles, handmodel.cpp:141-146
+            // one unconditional LDS read per lane (per-lane branches would serialise three
+            // read round trips): TWS (fingermodel.cpp:91), ANG, ROT, digit angles
+            // (handmodel.cpp:141-146)
+            const double th = f.th[l < 3 ? l : 6 + (l - 3)];
+            const double a = deg2rad(l == 0 ? th + 180 : th);
             double s, c;
             if (OUTLINE_TRIG) {
                 const SinCos r = sincos_outline(a);
@@ -327,13 +328,22 @@ __device__ __forceinline__ void fk_wave_t(FkSm &f, const DevHand *__restrict__ H
     }
     wave_sync();
     // spheres (fingermodel.cpp:208-267, thumbmodel.cpp:227-274): 144 (sphere, coord)
-    // items over the wave, weights from the hand tables; cols(1,2) *= -1 (handmodel.cpp:288)
+    // items over the wave, weights from the hand tables; cols(1,2) *= -1 (handmodel.cpp:288).
+    // Every item's joint reads are issued first (unconditional; the third item of lanes
+    // >= 16 reads a valid clamped entry), so the three items share one LDS round trip.
+    double ja[3], jb[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        const int it = l + 64 * q, r = (it < 3 * HPE_NS) ? it - 3 * (it / 3) : 0;
+        ja[q] = f.J[sd[q]][sa[q]][r];
+        jb[q] = f.J[sd[q]][sa[q] + 1][r];
+    }
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
         const int it = l + 64 * q;
         if (it < 3 * HPE_NS) {
-            const int s = it / 3, r = it - 3 * (it / 3), d = sd[q], a = sa[q];
-            const double v = swa[q] * f.J[d][a][r] + swb[q] * f.J[d][a + 1][r];
+            const int s = it / 3, r = it - 3 * (it / 3);
+            const double v = swa[q] * ja[q] + swb[q] * jb[q];
             const double vs = (r == 0) ? v : v * -1;
             f.S[s][r] = vs;
             f.Sp[r][s] = (float)vs;
@@ -494,8 +504,13 @@ __device__ __forceinline__ DepthG depth_issue(const FkSm &f, int i, const DevObs
     DepthG d;
     d.in = dx >= 0 && dx < HPE_IMG_W && dy >= 0 && dy < HPE_IMG_H;  // NaN: off-image
     const int pix = d.in ? (int)dy * HPE_IMG_W + (int)dx : 0;
+#ifdef HPE_DIAG_NO_GATHER  // diagnostic timing build only: results invalid
+    d.djc = (double)(pix & 7);
+    d.dtp = (float)(pix & 3);
+#else
     d.djc = gp(o.depth)[pix];
     d.dtp = gp(o.dt)[pix];
+#endif
     d.z = z;
     d.r = H->radii[i];
     return d;

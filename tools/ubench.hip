@@ -149,7 +149,7 @@ __global__ __launch_bounds__(HPE_NT) void k_ubench_block(const DevHand *Hg, DevO
     if (t < 26) sm.fk.th[t] = 5.0 + t;
     __syncthreads();
     const DevHand *H = &sm.hand;
-    const CloudView cv = obs_cloud(o);
+    const CloudGlobal cv = obs_cloud(o);
     double acc = 0;
     unsigned long long t0, t1;
     // 11: eval_block<EV_COST, 512>
