@@ -537,7 +537,22 @@ __device__ __forceinline__ double depth_term(const FkSm &f, int i, const DevObs 
     return depth_finish(depth_issue(f, i, o, H), o, true);
 }
 
-// one of the 144 self-collision pairs (costfunc.cpp:150-193)
+// one of the 144 self-collision pairs (costfunc.cpp:150-193), as a load half and an
+// arithmetic half (the same operations as collide_term)
+struct CollPair {
+    double ax, ay, az, bx, by, bz, ra, rb;
+};
+__device__ __forceinline__ CollPair collide_load(const FkSm &f, int t, const DevHand *__restrict__ H) {
+    const int p = t / 36, k = t % 36;
+    const int a = 2 + 10 * p + k / 6, b = 2 + 10 * (p + 1) + k % 6;
+    return CollPair{f.S[a][0], f.S[a][1], f.S[a][2], f.S[b][0], f.S[b][1], f.S[b][2],
+                    H->radii[a], H->radii[b]};
+}
+__device__ __forceinline__ double collide_value(const CollPair &c) {
+    const double dx = c.bx - c.ax, dy = c.by - c.ay, dz = c.bz - c.az;
+    const double v = (c.rb + c.ra) - sqrt((dx * dx + dy * dy) + dz * dz);
+    return v > 0 ? v * v : 0.0;
+}
 __device__ __forceinline__ double collide_term(const FkSm &f, int t,
                                                const DevHand *__restrict__ H) {
     const int p = t / 36, k = t % 36;
@@ -835,8 +850,16 @@ __device__ __forceinline__ double eval_wave_frozen(FkSm &f, const DevObs &o,
     sc.lap(15);
     double al = align_frozen(f, cv, H, match, l, 64);
     sc.lap(16);
-    double co = collide_term(f, l, H) + collide_term(f, l + 64, H) +
-                ((l < 16) ? collide_term(f, l + 128, H) : 0.0);
+    // three pairs per lane (the third for lanes 0..15, computed by every lane at a clamped
+    // index and selected): every LDS read of the three is issued before any is used, so
+    // they share one round trip, and the sum is complete before depth_finish's wait for
+    // the gathers (the empty asm uses it; asm statements keep their order)
+    CollPair cp[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) cp[k] = collide_load(f, k < 2 ? l + 64 * k : ((l < 16) ? l + 128 : l), H);
+    asm volatile("" ::"v"(cp[0].ax), "v"(cp[1].ax), "v"(cp[2].ax));
+    double co = collide_value(cp[0]) + collide_value(cp[1]) + ((l < 16) ? collide_value(cp[2]) : 0.0);
+    asm volatile("" ::"v"(co));
     double dep = depth_finish(dg, o, l < HPE_NS);
     sc.lap(17);
     wave_sum3(al, dep, co);
