@@ -738,19 +738,50 @@ __device__ __forceinline__ double align_frozen(const FkSm &f, const CV &cv,
                                                const DevHand *__restrict__ H,
                                                const int32_t *__restrict__ match, int lane0,
                                                int stride) {
-    // fixed trip count of 4 points per lane per chunk, predicated (no divergent tail)
+    // fixed trip count of 4 points per lane per chunk, predicated (no divergent tail).
+    // The four points' reads are issued in two batches (match + point, then the matched
+    // sphere), each pinned by an empty asm that needs all of them: left to itself the
+    // compiler of a kernel at the VGPR cap (k_refine) ran the points one after another,
+    // five dependent LDS round trips each.  Same operations per point as align_one.
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
     for (int base = 0; base < cv.n; base += 4 * stride) {
-        const int p0 = base + lane0, p1 = p0 + stride, p2 = p1 + stride, p3 = p2 + stride;
         const int n1 = cv.n - 1;
-        const double e0 = align_one(f, cv, H, match, min(p0, n1));
-        const double e1 = align_one(f, cv, H, match, min(p1, n1));
-        const double e2 = align_one(f, cv, H, match, min(p2, n1));
-        const double e3 = align_one(f, cv, H, match, min(p3, n1));
-        a0 += (p0 < cv.n) ? e0 : 0.0;
-        a1 += (p1 < cv.n) ? e1 : 0.0;
-        a2 += (p2 < cv.n) ? e2 : 0.0;
-        a3 += (p3 < cv.n) ? e3 : 0.0;
+        int p[4], id[4];
+        double px[4], py[4], pz[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            p[k] = base + lane0 + k * stride;
+            const int q = min(p[k], n1);
+            id[k] = match[q];
+            px[k] = cv.cx[q];
+            py[k] = cv.cy[q];
+            pz[k] = cv.cz[q];
+        }
+        asm volatile("" : "+v"(id[0]), "+v"(id[1]), "+v"(id[2]), "+v"(id[3]), "+v"(px[0]),
+                     "+v"(px[1]), "+v"(px[2]), "+v"(px[3]), "+v"(py[0]), "+v"(py[1]),
+                     "+v"(py[2]), "+v"(py[3]), "+v"(pz[0]), "+v"(pz[1]), "+v"(pz[2]), "+v"(pz[3]));
+        double sx[4], sy[4], sz[4], sr[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            sx[k] = f.S[id[k]][0];
+            sy[k] = f.S[id[k]][1];
+            sz[k] = f.S[id[k]][2];
+            sr[k] = H->radii[id[k]];
+        }
+        asm volatile("" : "+v"(sx[0]), "+v"(sx[1]), "+v"(sx[2]), "+v"(sx[3]), "+v"(sy[0]),
+                     "+v"(sy[1]), "+v"(sy[2]), "+v"(sy[3]), "+v"(sz[0]), "+v"(sz[1]),
+                     "+v"(sz[2]), "+v"(sz[3]), "+v"(sr[0]), "+v"(sr[1]), "+v"(sr[2]), "+v"(sr[3]));
+        double e[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const double dx = px[k] - sx[k], dy = py[k] - sy[k], dz = pz[k] - sz[k];
+            const double r = sqrt((dx * dx + dy * dy) + dz * dz) - sr[k];
+            e[k] = r * r;
+        }
+        a0 += (p[0] < cv.n) ? e[0] : 0.0;
+        a1 += (p[1] < cv.n) ? e[1] : 0.0;
+        a2 += (p[2] < cv.n) ? e[2] : 0.0;
+        a3 += (p[3] < cv.n) ? e[3] : 0.0;
     }
     return (a0 + a1) + (a2 + a3);
 }

@@ -137,6 +137,121 @@ __global__ void k_ubench(const DevHand *Hg, DevObs o, int32_t *match_g, double *
     t1 = now();
     acc += z;
     if (t == 0) out[10] = (t1 - t0) / REPS;
+    // 15: fk_wave + depth_issue + depth_finish (the FK -> gather chain, nothing overlapped)
+    t0 = now();
+    for (int r = 0; r < REPS; ++r) {
+        if (t < 26) f.th[t] += 1e-3;
+        wave_sync();
+        fk_wave(f, &hs);
+        const DepthG dg = depth_issue(f, t, o, &hs);
+        acc += depth_finish(dg, o, t < HPE_NS);
+    }
+    t1 = now();
+    if (t == 0) out[15] = (t1 - t0) / REPS;
+    // 16: fk_wave + align_frozen
+    t0 = now();
+    for (int r = 0; r < REPS; ++r) {
+        if (t < 26) f.th[t] += 1e-3;
+        wave_sync();
+        fk_wave(f, &hs);
+        acc += align_frozen(f, cv, &hs, mt, t, 64);
+    }
+    t1 = now();
+    if (t == 0) out[16] = (t1 - t0) / REPS;
+    // 17: fk_wave + depth_issue + align_frozen + depth_finish (no collision, no sum)
+    t0 = now();
+    for (int r = 0; r < REPS; ++r) {
+        if (t < 26) f.th[t] += 1e-3;
+        wave_sync();
+        fk_wave(f, &hs);
+        const DepthG dg = depth_issue(f, t, o, &hs);
+        double al = align_frozen(f, cv, &hs, mt, t, 64);
+        acc += al + depth_finish(dg, o, t < HPE_NS);
+    }
+    t1 = now();
+    if (t == 0) out[17] = (t1 - t0) / REPS;
+    // 18: fk_wave_t<FK_TRANSLATE> (no trig, no chain: joints from X + spheres)
+    __shared__ FkX X;
+    fk_wave_t<FK_STORE_X>(f, &hs, &X);
+    t0 = now();
+    for (int r = 0; r < REPS; ++r) {
+        if (t < 26) f.th[t] += 1e-3;
+        wave_sync();
+        fk_wave_t<FK_TRANSLATE>(f, &hs, &X);
+    }
+    t1 = now();
+    if (t == 0) out[18] = (t1 - t0) / REPS;
+    // 19: fp64 a / 180.0 dependent chain
+    double dv = 1.0 + t;
+    t0 = now();
+    for (int r = 0; r < REPS; ++r) dv = dv / 180.0 + 3.0;
+    t1 = now();
+    acc += dv;
+    if (t == 0) out[19] = (t1 - t0) / REPS;
+    // 20: the trig phase of fk_wave alone (th LDS read, deg2rad, sincos, LDS write, sync)
+    t0 = now();
+    for (int r = 0; r < REPS; ++r) {
+        if (t < 23) {
+            const double th = f.th[t < 3 ? t : 6 + (t - 3)];
+            const double a = deg2rad(t == 0 ? th + 180 : th);
+            double s, c;
+            sincos(a, &s, &c);
+            f.sn[t] = s;
+            f.cs[t] = c;
+        }
+        wave_sync();
+        if (t < 26) f.th[t] += f.sn[t % 23] * 1e-30;
+        wave_sync();
+    }
+    t1 = now();
+    if (t == 0) out[20] = (t1 - t0) / REPS;
+    // 21: fk + depth + align + collision (batched loads), no wave sum
+    t0 = now();
+    for (int r = 0; r < REPS; ++r) {
+        if (t < 26) f.th[t] += 1e-3;
+        wave_sync();
+        fk_wave(f, &hs);
+        const DepthG dg = depth_issue(f, t, o, &hs);
+        double al = align_frozen(f, cv, &hs, mt, t, 64);
+        CollPair cp[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) cp[k] = collide_load(f, k < 2 ? t + 64 * k : ((t < 16) ? t + 128 : t), &hs);
+        asm volatile("" ::"v"(cp[0].ax), "v"(cp[1].ax), "v"(cp[2].ax));
+        double co = collide_value(cp[0]) + collide_value(cp[1]) + ((t < 16) ? collide_value(cp[2]) : 0.0);
+        asm volatile("" ::"v"(co));
+        acc += (al + depth_finish(dg, o, t < HPE_NS)) + co;
+    }
+    t1 = now();
+    if (t == 0) out[21] = (t1 - t0) / REPS;
+    // 22: eval_wave_frozen's sequence written out (21 + wave_sum3)
+    t0 = now();
+    for (int r = 0; r < REPS; ++r) {
+        if (t < 26) f.th[t] += 1e-3;
+        wave_sync();
+        fk_wave(f, &hs);
+        const DepthG dg = depth_issue(f, t, o, &hs);
+        double al = align_frozen(f, cv, &hs, mt, t, 64);
+        CollPair cp[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) cp[k] = collide_load(f, k < 2 ? t + 64 * k : ((t < 16) ? t + 128 : t), &hs);
+        asm volatile("" ::"v"(cp[0].ax), "v"(cp[1].ax), "v"(cp[2].ax));
+        double co = collide_value(cp[0]) + collide_value(cp[1]) + ((t < 16) ? collide_value(cp[2]) : 0.0);
+        asm volatile("" ::"v"(co));
+        double dep = depth_finish(dg, o, t < HPE_NS);
+        wave_sum3(al, dep, co);
+        acc += (al * o.lambda + dep) + co;
+    }
+    t1 = now();
+    if (t == 0) out[22] = (t1 - t0) / REPS;
+    // 23: eval_wave_frozen again (order effects)
+    t0 = now();
+    for (int r = 0; r < REPS; ++r) {
+        if (t < 26) f.th[t] += 1e-3;
+        wave_sync();
+        acc += eval_wave_frozen(f, o, cv, &hs, mt);
+    }
+    t1 = now();
+    if (t == 0) out[23] = (t1 - t0) / REPS;
     sink[t] = acc;
 }
 
@@ -233,20 +348,24 @@ int main() {
     double *sink;
     hipMalloc(&sink, sizeof(double) * 1024);
     unsigned long long *dout;
-    hipMalloc(&dout, sizeof(unsigned long long) * 16);
+    hipMalloc(&dout, sizeof(unsigned long long) * 32);
     const char *names[] = {"fk_wave (H in LDS)", "fk_wave (H in HBM)", "eval_wave_frozen N=250",
                            "wave_sum3", "depth_term (48 lanes, gathers)", "align_frozen N=250",
                            "collision 144 pairs", "dependent global load (L2)",
                            "sincos f64 (dependent)", "sqrt f64 (dependent)",
                            "16 dependent f64 mul+add", "eval_block<COST,512> N=250",
-                           "search_align<512> N=250", "block_sum3<512>", "fk (wave 0) + syncs"};
+                           "search_align<512> N=250", "block_sum3<512>", "fk (wave 0) + syncs",
+                           "fk + depth (no overlap)", "fk + align_frozen", "fk + depth + align",
+                           "fk TRANSLATE (joints+spheres)", "f64 a/180 (dependent)",
+                           "trig phase alone", "fk+depth+align+coll", "written-out frozen eval",
+                           "eval_wave_frozen again"};
     for (int rep = 0; rep < 3; ++rep) {
         hipLaunchKernelGGL(k_ubench, dim3(1), dim3(256), 0, 0, dh, o, dm, sink, dout);
         hipLaunchKernelGGL(k_ubench_block, dim3(1), dim3(HPE_NT), 0, 0, dh, o, sink, dout);
         hipDeviceSynchronize();
     }
-    unsigned long long out[16];
+    unsigned long long out[32];
     hipMemcpy(out, dout, sizeof(out), hipMemcpyDeviceToHost);
-    for (int k = 0; k < 15; ++k) printf("%-34s %8llu cycles\n", names[k], out[k]);
+    for (int k = 0; k < 24; ++k) printf("%-34s %8llu cycles\n", names[k], out[k]);
     return 0;
 }
