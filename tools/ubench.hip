@@ -18,7 +18,7 @@ __device__ __forceinline__ unsigned long long now() {
 }
 
 // out[k] = average cycles of test k
-__global__ void k_ubench(const DevHand *Hg, DevObs o, int32_t *match_g, double *sink,
+__global__ __launch_bounds__(256) void k_ubench(const DevHand *Hg, DevObs o, int32_t *match_g, double *sink,
                          unsigned long long *out) {
     __shared__ FkSm f;
     __shared__ DevHand hs;
@@ -349,6 +349,7 @@ int main() {
     hipMalloc(&sink, sizeof(double) * 1024);
     unsigned long long *dout;
     hipMalloc(&dout, sizeof(unsigned long long) * 32);
+    hipMemset(dout, 0, sizeof(unsigned long long) * 32);
     const char *names[] = {"fk_wave (H in LDS)", "fk_wave (H in HBM)", "eval_wave_frozen N=250",
                            "wave_sum3", "depth_term (48 lanes, gathers)", "align_frozen N=250",
                            "collision 144 pairs", "dependent global load (L2)",
