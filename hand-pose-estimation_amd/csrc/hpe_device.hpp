@@ -179,6 +179,33 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// fp64 sqrt, bit-identical to the compiler's correctly rounded expansion of sqrt(): for
+// 2^-767 <= x < inf that expansion scales by 2^0 (its v_ldexp pair and the 0 / inf class
+// select are identities), so hpe_sqrt_nr runs the same rsq + Newton fma sequence without
+// them; every other input (0, tiny, negative, inf, NaN) is recomputed with sqrt() itself
+// on a branch the cost terms' squared distances practically never enter (callers with
+// several roots fix them up behind ONE branch, so the roots stay one basic block).
+// tools/sqrt_check.hip compares hpe_sqrt with sqrt bitwise.
+__device__ __forceinline__ bool hpe_sqrt_direct(double x) {
+    return x >= 0x1p-767 && x < __builtin_inf();
+}
+__device__ __forceinline__ double hpe_sqrt_nr(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = y * 0.5;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    double d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, x);
+    return __builtin_fma(d, h, g);
+}
+__device__ __forceinline__ double hpe_sqrt(double x) {
+    double g = hpe_sqrt_nr(x);
+    if (!hpe_sqrt_direct(x)) g = sqrt(x);
+    return g;
+}
+
 __device__ __forceinline__ double deg2rad(double a) {
     return a / 180.0 * 3.141592653589793115997963468544185161590576171875;  // fingermodel.cpp:203
 }
@@ -548,9 +575,12 @@ __device__ __forceinline__ CollPair collide_load(const FkSm &f, int t, const Dev
     return CollPair{f.S[a][0], f.S[a][1], f.S[a][2], f.S[b][0], f.S[b][1], f.S[b][2],
                     H->radii[a], H->radii[b]};
 }
-__device__ __forceinline__ double collide_value(const CollPair &c) {
+__device__ __forceinline__ double collide_d2(const CollPair &c) {
     const double dx = c.bx - c.ax, dy = c.by - c.ay, dz = c.bz - c.az;
-    const double v = (c.rb + c.ra) - sqrt((dx * dx + dy * dy) + dz * dz);
+    return (dx * dx + dy * dy) + dz * dz;
+}
+__device__ __forceinline__ double collide_value(const CollPair &c, double root) {
+    const double v = (c.rb + c.ra) - root;
     return v > 0 ? v * v : 0.0;
 }
 __device__ __forceinline__ double collide_term(const FkSm &f, int t,
@@ -730,7 +760,7 @@ __device__ __forceinline__ double align_one(const FkSm &f, const CV &cv,
     const int idx = match[p];
     const double dx = cv.cx[p] - f.S[idx][0], dy = cv.cy[p] - f.S[idx][1],
                  dz = cv.cz[p] - f.S[idx][2];
-    const double e = sqrt((dx * dx + dy * dy) + dz * dz) - H->radii[idx];
+    const double e = hpe_sqrt((dx * dx + dy * dy) + dz * dz) - H->radii[idx];
     return e * e;
 }
 template <class CV>
@@ -771,11 +801,21 @@ __device__ __forceinline__ double align_frozen(const FkSm &f, const CV &cv,
         asm volatile("" : "+v"(sx[0]), "+v"(sx[1]), "+v"(sx[2]), "+v"(sx[3]), "+v"(sy[0]),
                      "+v"(sy[1]), "+v"(sy[2]), "+v"(sy[3]), "+v"(sz[0]), "+v"(sz[1]),
                      "+v"(sz[2]), "+v"(sz[3]), "+v"(sr[0]), "+v"(sr[1]), "+v"(sr[2]), "+v"(sr[3]));
-        double e[4];
+        double d2[4], rt[4], e[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const double dx = px[k] - sx[k], dy = py[k] - sy[k], dz = pz[k] - sz[k];
-            const double r = sqrt((dx * dx + dy * dy) + dz * dz) - sr[k];
+            d2[k] = (dx * dx + dy * dy) + dz * dz;
+            rt[k] = hpe_sqrt_nr(d2[k]);
+        }
+        if (!(hpe_sqrt_direct(d2[0]) && hpe_sqrt_direct(d2[1]) && hpe_sqrt_direct(d2[2]) &&
+              hpe_sqrt_direct(d2[3]))) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) rt[k] = hpe_sqrt_direct(d2[k]) ? rt[k] : sqrt(d2[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const double r = rt[k] - sr[k];
             e[k] = r * r;
         }
         a0 += (p[0] < cv.n) ? e[0] : 0.0;
@@ -889,7 +929,18 @@ __device__ __forceinline__ double eval_wave_frozen(FkSm &f, const DevObs &o,
 #pragma unroll
     for (int k = 0; k < 3; ++k) cp[k] = collide_load(f, k < 2 ? l + 64 * k : ((l < 16) ? l + 128 : l), H);
     asm volatile("" ::"v"(cp[0].ax), "v"(cp[1].ax), "v"(cp[2].ax));
-    double co = collide_value(cp[0]) + collide_value(cp[1]) + ((l < 16) ? collide_value(cp[2]) : 0.0);
+    double d2[3], rt[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        d2[k] = collide_d2(cp[k]);
+        rt[k] = hpe_sqrt_nr(d2[k]);
+    }
+    if (!(hpe_sqrt_direct(d2[0]) && hpe_sqrt_direct(d2[1]) && hpe_sqrt_direct(d2[2]))) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) rt[k] = hpe_sqrt_direct(d2[k]) ? rt[k] : sqrt(d2[k]);
+    }
+    double co = collide_value(cp[0], rt[0]) + collide_value(cp[1], rt[1]) +
+                ((l < 16) ? collide_value(cp[2], rt[2]) : 0.0);
     asm volatile("" ::"v"(co));
     double dep = depth_finish(dg, o, l < HPE_NS);
     sc.lap(17);
