@@ -906,14 +906,14 @@ __device__ __forceinline__ double eval_block(Smem &sm, const DevObs &o, const CV
 // the total.
 // Xt != nullptr: f.th differs from the theta of Xt only in the global position
 // (FK_TRANSLATE).
-template <class CV>
+template <bool OUTLINE_TRIG = false, class CV>
 __device__ __forceinline__ double eval_wave_frozen(FkSm &f, const DevObs &o,
                                                    const CV &cv,
                                                    const DevHand *__restrict__ H,
                                                    const int32_t *__restrict__ match,
                                                    FkX *Xt = nullptr) {
     if (Xt) fk_wave_t<FK_TRANSLATE>(f, H, Xt);
-    else fk_wave(f, H);
+    else fk_wave<OUTLINE_TRIG>(f, H);
     StampClock sc;
     sc.start();
     const int l = threadIdx.x & 63;

@@ -1186,7 +1186,7 @@ __device__ __forceinline__ void eval_nodes(RefineSm &rs, int nn, const DevObs &o
     if (!MW) {
         if (w < nn) {
             wave_sync();
-            const double f = eval_wave_frozen(rs.w[w], o, cv, H, match, Xt);
+            const double f = eval_wave_frozen<true>(rs.w[w], o, cv, H, match, Xt);
             if (l == 0) rs.f[w] = f;
         }
         REF_TS(rs.ts_n, 9);  // wave 0's node done
@@ -1455,7 +1455,7 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
             if (w == 0) {
                 if (l < HPE_DOF) rs.w[0].th[l] = rs.x0[l];
                 wave_sync();
-                fk_wave_t<FK_STORE_X>(rs.w[0], H, &rs.X);
+                fk_wave_t<FK_STORE_X, true>(rs.w[0], H, &rs.X);
             }
             __syncthreads();
             Xt = &rs.X;
@@ -1471,7 +1471,7 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
                 __syncthreads();
                 if (w == 0) {
                     if (Xt) fk_wave_t<FK_TRANSLATE>(rs.base, H, Xt);
-                    else fk_wave(rs.base, H);
+                    else fk_wave<true>(rs.base, H);
                 }
                 __syncthreads();
             }
