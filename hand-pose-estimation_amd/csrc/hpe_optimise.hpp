@@ -131,7 +131,7 @@ __global__ __launch_bounds__(RF_NT) void k_opt_descent(DevOpt op, const DevObs *
         if (m == 0) {  // f_k = cal_cost2(ctheta, matchId, true)
             if (t < HPE_DOF) rs.base.th[t] = rs.x0[t];
             __syncthreads();
-            if (w == 0) fk_wave(rs.base, H);
+            if (w == 0) fk_wave<true>(rs.base, H);
             __syncthreads();
             const DepthG dg = depth_issue_w0(rs.base, o, H);
             double al = search_align<RF_NT, true>(rs.base, cv, H, match, load_pt(cv, t));
@@ -145,7 +145,7 @@ __global__ __launch_bounds__(RF_NT) void k_opt_descent(DevOpt op, const DevObs *
         if (w < 2) {  // cal_gradient: theta +/- eps on coordinate sel, frozen matchId
             if (l < HPE_DOF) rs.w[w].th[l] = (l == sel) ? (w ? rs.x0[l] - e5 : rs.x0[l] + e5) : rs.x0[l];
             wave_sync();
-            const double f = eval_wave_frozen(rs.w[w], o, cv, H, match);
+            const double f = eval_wave_frozen<true>(rs.w[w], o, cv, H, match);
             if (l == 0) rs.f[w] = f;
         }
         __syncthreads();
