@@ -752,17 +752,7 @@ __device__ __forceinline__ double search_align(const FkSm &f, const CV &cv,
 }
 
 // Alignment with frozen correspondences (cal_cost2(..., compute_corr=false)) over
-// `stride` lanes starting at `lane0`; four points in flight per lane.
-template <class CV>
-__device__ __forceinline__ double align_one(const FkSm &f, const CV &cv,
-                                            const DevHand *__restrict__ H,
-                                            const int32_t *__restrict__ match, int p) {
-    const int idx = match[p];
-    const double dx = cv.cx[p] - f.S[idx][0], dy = cv.cy[p] - f.S[idx][1],
-                 dz = cv.cz[p] - f.S[idx][2];
-    const double e = hpe_sqrt((dx * dx + dy * dy) + dz * dz) - H->radii[idx];
-    return e * e;
-}
+// `stride` lanes starting at `lane0`: per point e = |p - S[m]| - r[m], sum of e^2.
 template <class CV>
 __device__ __forceinline__ double align_frozen(const FkSm &f, const CV &cv,
                                                const DevHand *__restrict__ H,
@@ -772,7 +762,7 @@ __device__ __forceinline__ double align_frozen(const FkSm &f, const CV &cv,
     // The four points' reads are issued in two batches (match + point, then the matched
     // sphere), each pinned by an empty asm that needs all of them: left to itself the
     // compiler of a kernel at the VGPR cap (k_refine) ran the points one after another,
-    // five dependent LDS round trips each.  Same operations per point as align_one.
+    // five dependent LDS round trips each.
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
     for (int base = 0; base < cv.n; base += 4 * stride) {
         const int n1 = cv.n - 1;
