@@ -255,12 +255,19 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
                                                     double W1, double C1, double C2,
                                                     InboxCounts kin) {
     BLK_TS(g, 0);
+    // every argument word round 1 needs, loaded at entry as one batch: left alone the
+    // compiler fetched g and the gmin / sig / link / bounds pointers in a second scalar
+    // round trip behind the first one's wait, ahead of every global load of the round
+    // (a non-volatile asm: it touches no memory, so later loads keep their scalar form)
+    int z0 = 0;
+    asm("" : "+s"(z0) : "s"(g), "s"(sw.gmin), "s"(sw.sig), "s"(sw.outl), "s"(sw.bounds),
+        "s"(sw.xh), "s"(sw.pch), "s"(sw.pb), "s"(sw.v), "s"(sw.inbox), "s"(sw.P), "s"(sw.K));
     StampClock sc;
     sc.begin();
     const DevObs o = *og;  // the selected frame (device-resident: graph-stable args)
     __shared__ Smem sm;
     __shared__ double ib[2][IB_KMAX][IB_FIELDS];
-    const int i = blockIdx.x, t = threadIdx.x, P = sw.P, K = sw.K;
+    const int i = blockIdx.x + z0, t = threadIdx.x, P = sw.P, K = sw.K;
     // valid slots of this receiver's kept (0) / rebuilt (1) inbox: only these are read
     const int k0 = (P <= KIN_MAX) ? kin.k0[i] : K, k1 = (P <= KIN_MAX) ? kin.k1[i] : K;
     // Round 1: every load of the generation is issued before any value is used (one
