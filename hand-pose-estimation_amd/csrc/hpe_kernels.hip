@@ -827,10 +827,15 @@ __global__ __launch_bounds__(PW_NT) void k_pso_init_w(DevSwarm sw, const double 
 __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *__restrict__ og,
                                                      const DevHand *__restrict__ Hg, int g,
                                                      double W1, double C1, double C2) {
+    // every argument word loaded at entry in one batch (see k_pso_gen)
+    int z0 = 0;
+    asm("" : "+s"(z0) : "s"(g), "s"(sw.gmin), "s"(sw.sig), "s"(sw.outl), "s"(sw.bounds),
+        "s"(sw.xh), "s"(sw.pch), "s"(sw.pb), "s"(sw.v), "s"(sw.inbox), "s"(sw.ibtc),
+        "s"(sw.P), "s"(sw.K));
     const DevObs o = *og;
     __shared__ DevHand hs;
     __shared__ FkSm fks[PW_WPB];
-    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    const int t = threadIdx.x + z0, w = t >> 6, l = t & 63;
     const int i = blockIdx.x * PW_WPB + w, P = sw.P, K = sw.K;
     const bool valid = i < P;
     const int ic = valid ? i : P - 1;

@@ -1,5 +1,5 @@
 # A/B several in-tree builds (HPE_LIB_VARIANT files) on the default bench config.
-# Usage (on the box): bash tools/gpu_ab_multi.sh rounds lib1.so lib2.so ...
+# Usage (on the box): [BENCH_ARGS="--config p4096"] bash tools/gpu_ab_multi.sh rounds lib1.so lib2.so ...
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 R=$1; shift
@@ -7,7 +7,7 @@ O=gpurun_out/abm
 rm -rf $O; mkdir -p $O
 for r in $(seq 1 $R); do
   for v in "$@"; do
-    HPE_LIB_VARIANT=$v timeout -k 10 200 python bench.py --steps 40 --no-cpu-baseline > $O/bench_$(basename $v .so)_$r.log 2>&1 || exit 1
+    HPE_LIB_VARIANT=$v timeout -k 10 200 python bench.py --steps 40 --no-cpu-baseline $BENCH_ARGS > $O/bench_$(basename $v .so)_$r.log 2>&1 || exit 1
   done
 done
 python3 - <<'PY'
