@@ -43,6 +43,9 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "hand-pose-estimation_amd"))
 
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
+# the synthetic sequence: trajectory seed and mean reversion toward x0 (keeps the hand in
+# view); fixed from round 2 on so bench lines compare round over round
+TRAJ_SEED, TRAJ_REVERT = 0, 0.02
 FP32_PEAK_TFLOPS = 157.3  # vector fp32 (spec); the search is fp32 VALU, no MFMA
 
 CONFIGS = {  # name -> (particles, generations, BASELINE.json workload)
@@ -82,10 +85,20 @@ def parse():
                          "the next frame from host depth on the GPU, overlapped)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--seed", type=int, default=0, help="trajectory seed")
+    ap.add_argument("--seed", type=int, default=TRAJ_SEED, help="trajectory seed")
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                    help="process group for --gpus N > 1 (nccl = RCCL over xGMI; gloo: the "
+                         "per-frame exchange through host memory, a rehearsal mode)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="every rank uses cuda:0 (rehearse N ranks on a one-GPU box; with "
+                         "--backend gloo)")
     ap.add_argument("--frames", default=os.environ.get("HPE_FRAMES_DIR"),
                     help="directory of MSRA-style *_depth.bin frames (headerless float32 mm, "
                          "240x320) to track instead of the synthetic sequence")
+    ap.add_argument("--dump", default=None,
+                    help="test mode: each rank saves its state after every frame of the first "
+                         "pass (synchronising per frame) and rank 0 the first raw frame and x0, "
+                         "as .npy under this directory")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)
     a = ap.parse_args()
     P, G, _ = CONFIGS[a.config]
@@ -146,7 +159,7 @@ def cpu_baseline(args, recorded=None):
     if recorded is not None:  # the same recorded frames the GPU tracked
         raw, x_start = recorded, hpe.X0.copy()
     else:
-        poses = synth.trajectory(64, args.seed, revert=0.02)
+        poses = synth.trajectory(64, args.seed, revert=TRAJ_REVERT)
         raw = [oracle_np.render_depth_mm(nh, poses[f]) for f in range(len(poses))]
         x_start = poses[0].copy()
 
@@ -297,9 +310,14 @@ def main():
     from hpe import synth
     from hpe.dist import exchange_best, subswarm_seed
 
+    if args.same_device:
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     P, G = args.particles, args.generations
     hand = hpe.reference_hand(device=local)
@@ -316,7 +334,7 @@ def main():
                for fp in files[:n_frames]]
         poses = None  # no ground truth: x0 of test_full (testmodel.cpp:38-40)
     else:
-        poses = synth.trajectory(n_frames, args.seed, revert=0.02)
+        poses = synth.trajectory(n_frames, args.seed, revert=TRAJ_REVERT)
         raw = [np.ascontiguousarray(ctx.render_depth(th)) for th in poses]
     sizes = [len(hpe.preprocess_depth(d, True, ds)["cloud"]) for d in raw]
     if args.resident:  # frames preprocessed and resident in HBM before the timed region
@@ -333,6 +351,7 @@ def main():
     torch.cuda.synchronize()
     ext = torch.cuda.ExternalStream(lib.hpe_stream(ctx.h), device=f"cuda:{local}")
     gathered = torch.zeros(world * 27, dtype=torch.float64, device=f"cuda:{local}")
+    gathered_host = torch.zeros(world * 27, dtype=torch.float64)
     refine = 0 if args.no_refine else 1
 
     def step(f):
@@ -341,14 +360,34 @@ def main():
             ctx.check(lib.hpe_track_frame_dev(ctx.h, P, refine, C.c_void_p(state.data_ptr())))
         else:  # frame f tracked while frame f+1 is prepared inside its refine launch
             ctx.track_pipelined(P, refine, state.data_ptr(), raw[f + 1] if f + 1 < n_frames else None)
-        if world > 1:  # best-of-N exchange on the tracker's own stream (no host sync)
+        if world > 1 and args.backend == "nccl":
+            # best-of-N exchange on the tracker's own stream (no host sync)
             with torch.cuda.stream(ext):
                 exchange_best(state, gathered)
+        elif world > 1:  # gloo: through host memory (rehearsal mode, synchronous)
+            ctx.check(lib.hpe_sync(ctx.h))
+            hs = state.cpu()
+            exchange_best(hs, gathered_host)
+            state.copy_(hs)
 
+    dumped = []
+
+    def dump_state():
+        if args.dump:  # test mode (see --dump): one synchronisation per frame
+            ctx.check(lib.hpe_sync(ctx.h))
+            torch.cuda.synchronize()
+            dumped.append(state.cpu().numpy().copy())
+
+    if args.dump:
+        os.makedirs(args.dump, exist_ok=True)
+        if rank == 0:
+            np.save(os.path.join(args.dump, "raw0.npy"), raw[0])
+            np.save(os.path.join(args.dump, "x0.npy"), state[:26].cpu().numpy())
     if not args.resident:
         ctx.pipeline_begin(raw[0], True, ds)
     for f in range(args.warmup):
         step(f)
+        dump_state()
     ctx.check(lib.hpe_sync(ctx.h))
     torch.cuda.synchronize()
     # timed region: graph-replayed frames, nothing else on the tracker stream
@@ -361,16 +400,20 @@ def main():
         h0 = time.perf_counter()
         step(f)
         host_s += time.perf_counter() - h0
+        dump_state()
     ctx.check(lib.hpe_sync(ctx.h))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([el], dtype=torch.float64,
+                         device=f"cuda:{local}" if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     final = state.cpu().numpy()
+    if args.dump:
+        np.save(os.path.join(args.dump, f"states_rank{rank}.npy"), np.array(dumped))
     # per-frame device time: the same frames again with one event pair per frame on the
     # tracker stream (not in the timed region: each timing event adds a marker, ~5 us)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -410,7 +453,7 @@ def main():
     ctx.check(lib.hpe_refine_eval_count(ctx.h, C.byref(rev), 1))
     prof = {}
     for name, kid in (("k_pso_gen", 0), ("k_refine", 1), ("k_pso_init", 2), ("k_pso_final", 3),
-                      ("k_preprocess", 4), ("k_pso_loop", 7)):
+                      ("k_preprocess", 4)):
         nl = C.c_int32(0); tot = C.c_double(0); mn = C.c_double(0); mx = C.c_double(0)
         ctx.check(lib.hpe_profile_read_kernel(ctx.h, kid, C.byref(nl), C.byref(tot),
                                               C.byref(mn), C.byref(mx)))
@@ -426,27 +469,30 @@ def main():
     if rank == 0:
         n_pts = sizes[args.warmup]
         evals = P * (G + 1) * args.steps * world
-        # the PSO generations: one k_pso_loop launch per frame (G generations, grid-resident
-        # form) or one k_pso_gen launch per generation
-        loop = roofline_entry("k_pso_loop", prof, P * G, n_pts, lib_path, P)
         gen = roofline_entry("k_pso_gen", prof, P, n_pts, lib_path, P)
         ref_launches = prof["k_refine"]["launches"]
         ref = (roofline_entry("k_refine", prof, rev.value / ref_launches, n_pts, lib_path, P)
                if ref_launches and rev.value else None)
-        roof = dict(loop or gen or {})
+        kernels_rf = {"k_pso_gen": gen, "k_refine": ref}
+        # the dominant kernel: the most device time per frame (hipExtLaunchKernel events)
+        dom = max((k for k in kernels_rf if kernels_rf[k]),
+                  key=lambda k: prof[k]["total_ms"], default=None)
+        roof = dict(kernels_rf[dom]) if dom else {}
         if roof:
-            if loop:
-                roof["us_per_generation"] = loop["avg_launch_us"] / G
-            roof["note"] = ("algorithmic bytes per launch = evaluations per launch x (12N + 600) "
-                            "(SURVEY.md §8 d2), per-launch time from hipExtLaunchKernel events on "
-                            "the tracker stream; " + (
-                                f"k_pso_loop = the {G} generations of a frame in one grid-"
-                                "resident launch (one workgroup per particle, generations "
-                                "separated by data-tagged granule waits)" if loop else
-                                "k_pso_gen = one generation per launch") +
-                            "; latency-bound (one particle per workgroup, dependent "
-                            "generations), DESIGN.md §5")
+            roof["note"] = (
+                "dominant kernel by device time per frame; algorithmic bytes per launch = "
+                "evaluations per launch x (12N + 600) (SURVEY.md §8 d2), per-launch time from "
+                "hipExtLaunchKernel events on the tracker stream; " + (
+                    "k_pso_gen = one generation of the swarm per launch, one particle per "
+                    "workgroup" if dom == "k_pso_gen" else
+                    "k_refine = refine_init_pose as ONE workgroup (a serial chain of "
+                    "evaluations), plus the next frame's preparation workgroups") +
+                "; latency-bound (dependent generations / a serial line search), DESIGN.md §5")
             roof["limiter"] = "latency"
+        dominant = {"kernel": dom,
+                    "ms_per_frame": {k: prof[k]["total_ms"] / max(args.steps, 1)
+                                     for k in ("k_pso_gen", "k_refine", "k_pso_init",
+                                               "k_pso_final")}}
         line = {
             "metric": "particle-evals/sec + tracked FPS, 320x240 depth, 256p x 30gen",
             "value": evals / el,
@@ -457,7 +503,7 @@ def main():
             "ms_per_step": el / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": None,
+            "vs_baseline": None,  # set below from the same-run CPU baseline
             "dtype": "f32+f64",
             "data": (f"recorded: {n_frames} *_depth.bin frames from {args.frames}" if args.frames
                      else "synthetic: seeded 26-DOF trajectory rendered from the 48-sphere "
@@ -468,8 +514,14 @@ def main():
                                     "launch) + ") + "refine_init_pose + pso_evolve + "
                                     "cal_cost(bestp)"),
                        "particles": P, "generations": G, "maxiter": G + 1,
+                       "trajectory": (None if args.frames else
+                                      {"seed": args.seed, "revert": TRAJ_REVERT,
+                                       "frames": n_frames}),
                        "cloud_points": n_pts, "refine": bool(refine),
-                       "parallelism": f"subswarms x{world}, all-gather best per frame"},
+                       "parallelism": f"subswarms x{world}, all-gather best per frame"
+                                      + ("" if world == 1 else f" ({args.backend}"
+                                         + (", ranks sharing cuda:0)" if args.same_device
+                                            else ")"))},
             "tracked_fps": args.steps / el,
             "final_cost": float(final[26]),
             "tracking_err_mm": ({"sum_wrist_tips_mean": float(np.mean(errs)),
@@ -478,7 +530,8 @@ def main():
                                          "trajectory's true poses, second pass over the frames"}
                                 if errs else None),
             "roofline": roof or None,
-            "roofline_kernels": {"k_pso_loop": loop, "k_pso_gen": gen, "k_refine": ref},
+            "dominant_kernel": dominant,
+            "roofline_kernels": kernels_rf,
             "refine_evals_per_frame": rev.value / max(ref_launches, 1),
             "kernels": prof,
             "host_us_per_step": host_s / args.steps * 1e6,
@@ -489,6 +542,11 @@ def main():
             line["cpu_baseline"] = cb
             line["speedup_vs_cpu"] = {"particle_evals": line["value"] / cb["value"],
                                       "tracked_fps": line["tracked_fps"] / cb["tracked_fps"]}
+            # nothing published; its §2 baseline is the CPU restatement
+            # timed in the same run on the same host, so vs_baseline is GPU / that CPU path
+            line["vs_baseline"] = line["value"] / cb["value"]
+            line["vs_baseline_basis"] = ("cpu_baseline (BASELINE.md §2: no published number; "
+                                         "the oracle on this box's host cores, same workload)")
         print(json.dumps(line), flush=True)
     hand.ctx.close()
     if world > 1:

@@ -228,8 +228,8 @@ struct FkX {
     double x[15][5];
 };
 
-// ocml's fp64 sincos as an out-of-line call: inside a persistent loop (k_pso_loop) the
-// inlined version's ~20 polynomial constants are hoisted out of the loop and spilled.
+// ocml's fp64 sincos as an out-of-line call: inside the refine's loops the inlined
+// version's ~20 polynomial constants are hoisted out of the loop and spilled.
 struct SinCos {
     double s, c;
 };

@@ -429,321 +429,6 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
     sc.span(5);
 }
 
-// ---------------------------------------------------------------- grid-resident form
-// k_pso_loop runs generations 1..G of the workgroup form in ONE launch (P <= the CU count,
-// every workgroup resident; the host checks the occupancy).  The kernel boundary that
-// orders the generations of k_pso_gen becomes a wait on data-tagged granules: at the end
-// of generation g particle s publishes {tag (epoch, g, s), pbest cost} to gcell[g & 1][s]
-// and its pushes as GR_ROW granules per receiver, each with the same tag, by 16-B sc1
-// stores (write-through, untorn); generation g+1 of receiver i polls, with 16-B sc1 loads,
-// the P cost granules (the gmin reduction's inputs) and exactly the inbox slots that
-// generation g fills for it (in-degree of i under the kept and the rebuilt topology, from
-// the host-drawn links), until every tag matches.  No flag orders the payload: a granule
-// is valid by its own tag (MI355X_MICROARCH.md, hand-off table row 1).  Parity buffers:
-// a writer of generation g+2 has seen every cost granule of g+1, so every reader of g has
-// finished.  The epoch (k_pso_final bumps it) keeps an older call's granules from
-// matching.  Own x / v / pbest stay in registers across generations.  Every wait is
-// bounded (POLL_TICKS of the 100 MHz clock); a timeout sets sw.err, ends the launch
-// early, and k_pso_final then reports a NaN cost.
-#define POLL_TICKS 2000000ull  // 20 ms
-
-typedef unsigned int hpe_u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t gr_rsrc(const Gran *base) {
-    // raw buffer over the whole array (word 3: 32-bit data format, as for any raw access)
-    return __builtin_amdgcn_make_buffer_rsrc((void *)base, 0, 0x7fffffff, 0x00020000);
-}
-// aux 16 = SC1: the load is served from L2/memory, never from this CU's L1
-__device__ __forceinline__ Gran gr_load(__amdgpu_buffer_rsrc_t r, size_t idx) {
-    const hpe_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(idx * sizeof(Gran)), 0, 16);
-    Gran g;
-    g.tag = ((unsigned long long)v.y << 32) | v.x;
-    g.val = __hiloint2double((int)v.w, (int)v.z);
-    return g;
-}
-// one 16-B write-through store
-__device__ __forceinline__ void gr_store(__amdgpu_buffer_rsrc_t r, size_t idx, unsigned long long tag,
-                                         double val) {
-    hpe_u32x4 v;
-    v.x = (unsigned)tag;
-    v.y = (unsigned)(tag >> 32);
-    v.z = (unsigned)__double2loint(val);
-    v.w = (unsigned)__double2hiint(val);
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(idx * sizeof(Gran)), 0, 16);
-}
-__device__ __forceinline__ unsigned long long gr_tag(unsigned ep, int g, int s) {
-    return ((unsigned long long)ep << 32) | ((unsigned long long)(unsigned)g << 16) | (unsigned)s;
-}
-__device__ __forceinline__ size_t gib_index(const DevSwarm &sw, int par, int var, int r, int slot, int f) {
-    return ((((size_t)par * 2 + var) * sw.P + r) * sw.K + slot) * GR_ROW + f;
-}
-// link of pushing lane q (destination q / GR_ROW; var 1 = destinations 0..2)
-__device__ __forceinline__ Link load_link_gr(const DevSwarm &sw, int g, int s, int q, int tt, bool want) {
-    Link L;
-    L.ok = want && g < sw.G && q >= 0 && q < 6 * GR_ROW && tt >= 1;
-    const size_t k = L.ok ? ((size_t)tt * sw.P + s) * 3 + (q / GR_ROW) % 3 : 0;
-    L.raw = ((const long long *)sw.outl)[k];
-    return L;
-}
-// push field q % GR_ROW of particle s's generation-g row to its receiver (0: pbest cost)
-__device__ __forceinline__ void push_gran(const DevSwarm &sw, __amdgpu_buffer_rsrc_t rib, unsigned ep,
-                                          int g, int s, int q, const Link &L, double pc,
-                                          const double *row) {
-    const int r = L.ok ? (int)(L.raw & 0xffffffff) : -1;
-    if (r < 0) return;
-    const int dst = q / GR_ROW, f = q - GR_ROW * dst, var = dst < 3 ? 1 : 0;
-    gr_store(rib, gib_index(sw, g & 1, var, r, (int)(L.raw >> 32), f), gr_tag(ep, g, s),
-             f == 0 ? pc : row[f - 1]);
-}
-
-// generate_particles + initial evaluation (as k_pso_init), publishing generation 0 as
-// granules for k_pso_loop.
-__global__ __launch_bounds__(HPE_NT) void k_pso_init_gr(DevSwarm sw, const double *__restrict__ x0,
-                                                        const DevObs *__restrict__ og,
-                                                        const DevHand *__restrict__ Hg) {
-    const DevObs o = *og;
-    __shared__ Smem sm;
-    const int i = blockIdx.x, t = threadIdx.x;
-    const double hw = hand_word<HPE_NT>(Hg);
-    const DevHand *__restrict__ H = &sm.hand;
-    const unsigned ep = *sw.epoch;
-    const double *sd = sw.bounds + 2 * HPE_DOF;
-    const int q = t - 64;  // pushing lanes: waves 1..2 (3 destinations x GR_ROW), topology 1
-    const Link lk = load_link_gr(sw, 0, i, q, 1, q < 3 * GR_ROW);
-    const CloudGlobal cv = obs_cloud(o);
-    const Pt pre = load_pt(cv, t);
-    if (t < HPE_DOF) {  // particles = x0 + randn % std (PSO.cpp:67-72)
-        const size_t e = (size_t)i * HPE_DOF + t;
-        const double x = x0[t] + sw.normals[e] * sd[t];
-        sm.fk.th[t] = x;
-        sw.xh[e] = x;
-        sw.pb[e] = x;
-        sw.v[e] = 0.0;
-    }
-    hand_put<HPE_NT>(sm.hand, hw);
-    __syncthreads();
-    const double c = eval_block<EV_COST, HPE_NT>(sm, o, cv, H, nullptr, pre);
-    if (t == 0) {  // PSO.cpp:748-763
-        sw.pch[i] = c;
-        gmin_lower(sw, 0, i, c);
-        gr_store(gr_rsrc(sw.gcell), i, gr_tag(ep, 0, i), c);
-    }
-    push_gran(sw, gr_rsrc(sw.gib), ep, 0, i, q, lk, c, sm.fk.th);
-}
-
-__global__ __launch_bounds__(HPE_NT) void k_pso_loop(DevSwarm sw, const DevObs *__restrict__ og,
-                                                     const DevHand *__restrict__ Hg,
-                                                     double W1, double C1, double C2) {
-    const DevObs o = *og;
-    __shared__ Smem sm;
-    __shared__ double ib[2][IB_KMAX][IB_FIELDS];  // informant rows: [var][slot][2 + dim]
-    __shared__ uint8_t deg[PERSIST_MAX_G + 1];    // this receiver's in-degree per topology
-    __shared__ int pflag[2][HPE_NW];
-    __shared__ int bail;
-    const int i = blockIdx.x, t = threadIdx.x, P = sw.P, K = sw.K, G = sw.G;
-    const int w = t >> 6, l = t & 63;
-    const unsigned ep = *sw.epoch;
-    const __amdgpu_buffer_rsrc_t rib = gr_rsrc(sw.gib), rgc = gr_rsrc(sw.gcell);
-    stage_hand<HPE_NT>(sm.hand, Hg);
-    const DevHand *__restrict__ H = &sm.hand;
-    for (int k = t; k <= G; k += HPE_NT) deg[k] = sw.indeg[(size_t)k * P + i];
-    const CloudGlobal cv = obs_cloud(o);
-    const Pt pre = load_pt(cv, t);  // this thread's first cloud point (every generation)
-    const int q = t - 64;           // pushing lanes (waves 1..3)
-    // own state of generation 0 (wave 0, lane = dimension), kept in registers
-    double xo = 0, vo = 0, pbi = 0, lbt = 0, ubt = 0, pci = 0;
-    if (t < 64) {
-        const size_t ec = (size_t)i * HPE_DOF + (t < HPE_DOF ? t : HPE_DOF - 1);
-        xo = sw.xh[ec];
-        vo = sw.v[ec];
-        pbi = sw.pb[ec];
-        lbt = sw.bounds[ec - (size_t)i * HPE_DOF];
-        ubt = sw.bounds[ec - (size_t)i * HPE_DOF + HPE_DOF];
-        pci = sw.pch[i];
-    }
-    if (t == 0) bail = 0;
-    Sig sg = {1e100, 100, -1};  // sig of the previous generation (uniform, every thread)
-    __syncthreads();
-    for (int g = 1; g <= G; ++g) {
-        const int par = (g - 1) & 1;
-        const unsigned long long want = ((unsigned long long)ep << 16) | (unsigned)(g - 1);  // tag >> 16
-        // valid slots this generation: kept topology sg.topo (g >= 2), rebuilt topology g
-        const int n0 = (g >= 2) ? deg[sg.topo] : 0, n1 = deg[g];
-        const int self_lane = (K <= 15) ? 15 : 63;
-        // loads that do not wait for the previous generation
-        const Link lk1 = load_link_gr(sw, g, i, q, g + 1, q < 3 * GR_ROW);
-        if (t >= 64 && t < 64 + 2 * HPE_DOF) {  // wave 1: rp, rg of this generation
-            const int j = t - 64, d = j < HPE_DOF ? j : j - HPE_DOF;
-            sm.draws[j] = philox_u01(sw.seed, j < HPE_DOF ? ST_RP : ST_RG, g, i, d);
-        }
-        // ---- wait for generation g-1: wave 0 the P cost granules and both variants' cost
-        // granules (slot = lane), waves 1..7 the payload granules (fields 1..26) into LDS
-        double gv[PERSIST_MAX_P / 64], cst[2];
-        int csrc[2];
-        double fmn = 0;                      // gmin of g-1 (wave 0)
-        int infv[2] = {0, 0}, islv[2] = {-1, -1};  // informant under both variants (wave 0)
-        bool mine = false;
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        BLK_TS(g, 0);
-        for (int it = 0;; ++it) {
-            if (!mine) {
-                bool ok = true;
-                if (t < 64) {
-#pragma unroll
-                    for (int k = 0; k < PERSIST_MAX_P / 64; ++k) {
-                        const int s = min(l + 64 * k, P - 1);
-                        const Gran c = gr_load(rgc, (size_t)par * P + s);
-                        gv[k] = c.val;
-                        ok = ok && (l + 64 * k >= P || c.tag == gr_tag(ep, g - 1, s));
-                    }
-#pragma unroll
-                    for (int vr = 0; vr < 2; ++vr) {
-                        const int n = vr ? n1 : n0;
-                        const Gran c = gr_load(rib, gib_index(sw, par, vr, i, min(l, max(n - 1, 0)), 0));
-                        cst[vr] = c.val;
-                        csrc[vr] = (int)(c.tag & 0xffff);
-                        ok = ok && (l >= n || (c.tag >> 16) == want);
-                    }
-                } else {
-                    const int n = (n0 + n1) * (GR_ROW - 1), u0 = t - 64;
-                    Gran a[3];
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) {  // unconditional (clamped) loads
-                        const int u = min(u0 + k * (HPE_NT - 64), max(n - 1, 0));
-                        const int row = u / (GR_ROW - 1), f = 1 + u - row * (GR_ROW - 1);
-                        const int vr = row >= n0 ? 1 : 0;
-                        a[k] = gr_load(rib, gib_index(sw, par, vr, i, row - (vr ? n0 : 0), f));
-                    }
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) {
-                        const int u = u0 + k * (HPE_NT - 64);
-                        if (u < n) {
-                            const int row = u / (GR_ROW - 1), f = 1 + u - row * (GR_ROW - 1);
-                            const int vr = row >= n0 ? 1 : 0;
-                            ok = ok && (a[k].tag >> 16) == want;
-                            ib[vr][row - (vr ? n0 : 0)][1 + f] = a[k].val;
-                        }
-                    }
-                }
-                mine = __all(ok);
-                if (t < 64 && mine) {
-                    // wave 0's part has arrived: the gmin reduction and both variants'
-                    // informant argmins (:810-812) while the other waves may still wait
-                    double m = __builtin_nan("");
-#pragma unroll
-                    for (int k = 0; k < PERSIST_MAX_P / 64; ++k) m = (l + 64 * k < P) ? fmin(m, gv[k]) : m;
-                    m = fmin(m, dpp_f64<0xB1>(m));
-                    m = fmin(m, dpp_f64<0x4E>(m));
-                    m = fmin(m, dpp_f64<0x141>(m));
-                    m = fmin(m, dpp_f64<0x140>(m));
-                    fmn = fmin(fmin(readlane_f64(m, 0), readlane_f64(m, 16)),
-                               fmin(readlane_f64(m, 32), readlane_f64(m, 48)));
-#pragma unroll
-                    for (int vr = 0; vr < 2; ++vr) {
-                        const bool okv = l < (vr ? n1 : n0), self = l == self_lane;
-                        double v = okv ? cst[vr] : (self ? pci : __builtin_inf());
-                        const int idx = okv ? csrc[vr] : (self ? i : 0x7fffffff);
-                        if (v != v) v = __builtin_inf();
-                        if (K <= 15) row0_argmin_lex(v, idx, okv ? l : -1, infv[vr], islv[vr]);
-                        else wave_argmin_lex(v, idx, okv ? l : -1, infv[vr], islv[vr]);
-                    }
-                }
-            }
-            if (l == 0) pflag[it & 1][w] = mine;
-            if (t == 0 && !mine) {
-                const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-                if (now - t0 > POLL_TICKS ||
-                    ((it & 31) == 31 && __hip_atomic_load(sw.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-                    __hip_atomic_store(sw.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    bail = 1;
-                }
-            }
-            __syncthreads();
-            bool all = true;
-#pragma unroll
-            for (int k = 0; k < HPE_NW; ++k) all = all && pflag[it & 1][k];
-            if (all || bail) break;
-            if (!mine) __builtin_amdgcn_s_sleep(1);
-        }
-        if (bail) return;  // uniform: the launch ends early (sw.err is set)
-        BLK_TS(g, 1);
-        if (t < 64) {
-            // ---- end-of-generation update of g-1 (PSO.cpp:864-877) / initial gbest (:755-760)
-            Sig nsg;
-            if (g == 1) {
-                nsg.gcost = fmn < 1e100 ? fmn : 1e100;
-                nsg.count = 100;  // PSO.cpp:768
-                nsg.topo = -1;
-            } else {
-                const bool imp = fmn < sg.gcost;
-                nsg.gcost = imp ? fmn : sg.gcost;
-                nsg.count = imp ? 0 : sg.count + 1;
-                nsg.topo = sg.topo;
-            }
-            if (nsg.count > 0) nsg.topo = g;  // rebuilt when count > 0 (PSO.cpp:790)
-            if (i == 0 && t == 0) sw.sig[g] = nsg;
-            const int var = (nsg.topo == g) ? 1 : 0;
-            // ---- informant = first argmin of pbest cost over {i} U incoming (:810-812),
-            // computed for both variants above; the decision selects
-            const int inf = var ? infv[1] : infv[0], islot = var ? islv[1] : islv[0];
-            if (t == 0) {
-                sm.iscal[0] = nsg.topo;
-                sm.dscal[4] = pci;
-            }
-            if (t < HPE_DOF) sm.pbr[t] = pbi;  // pushed if x does not improve
-            sg = nsg;
-            // ---- velocity, position, check_constraints (PSO.cpp:824-842, 358-377); the
-            // draws and the informant rows are in LDS since the wait's last barrier
-            if (t < HPE_DOF) {
-                const double rp = sm.draws[t], rg = sm.draws[HPE_DOF + t];
-                double vn;
-                if (inf == i) {
-                    vn = W1 * vo + (C1 * rp) * (pbi - xo);
-                } else {
-                    const double pbn = ib[var][islot][2 + t];
-                    vn = (W1 * vo + (C1 * rp) * (pbi - xo)) + (C2 * rg) * (pbn - xo);
-                }
-                double xn = xo + vn;
-                const double xr = xn;
-                if (xr < lbt) { xn = lbt; vn = 0.; }
-                if (xr > ubt) { xn = lbt; vn = 0.; }  // above max -> MIN (PSO.cpp:372)
-                sw.xh[(size_t)g * P * HPE_DOF + (size_t)i * HPE_DOF + t] = xn;
-                sm.fk.th[t] = xn;
-                xo = xn;
-                vo = vn;
-            }
-            wave_sync();
-            fk_wave<true>(sm.fk, H);
-        }
-        __syncthreads();  // spheres, topology and own pbest cost published
-        const int topo = sm.iscal[0];
-        sg.topo = topo;  // every wave sizes the next generation's wait from it
-        BLK_TS(g, 2);
-        const double pcb = sm.dscal[4];
-        const Link lk0 = load_link_gr(sw, g, i, q, topo, q >= 3 * GR_ROW);
-        // ---- evaluation and pbest (PSO.cpp:848-861)
-        const double fx = eval_block<EV_COST, HPE_NT, false>(sm, o, cv, H, nullptr, pre, g);
-        BLK_TS(g, 3);
-        const bool better = fx < pcb;
-        const double pn = better ? fx : pcb;
-        if (t < HPE_DOF && better) pbi = sm.fk.th[t];
-        pci = pn;  // wave 0's copy is the one used
-        if (t == 0) {
-            sw.pch[(size_t)g * P + i] = pn;
-            gmin_lower(sw, g, i, pn);
-            gr_store(rgc, (size_t)(g & 1) * P + i, gr_tag(ep, g, i), pn);
-        }
-        // publish the pushes (granules; the row is this generation's x or the entry pbest)
-        // (sm.fk.th / sm.pbr are rewritten only after the next generation's wait, whose
-        // barriers follow these reads)
-        push_gran(sw, rib, ep, g, i, q, q < 3 * GR_ROW ? lk1 : lk0, pn, better ? sm.fk.th : sm.pbr);
-        BLK_TS(g, 4);
-    }
-    if (t < HPE_DOF) {  // own velocity and pbest for any later reader
-        sw.v[(size_t)i * HPE_DOF + t] = vo;
-        sw.pb[(size_t)i * HPE_DOF + t] = pbi;
-    }
-}
-
 // ---------------------------------------------------------------- wave-per-particle form
 // For swarms much larger than the CU count (BASELINE configs 4 and 5) one workgroup per
 // particle leaves the SIMDs idle during the single-wave FK and reductions; here each wave
@@ -976,9 +661,6 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
     __shared__ double gm[CH];
     __shared__ int tp[CH];
     const int t = threadIdx.x, G = sw.G, P = sw.P;
-    // a k_pso_loop wait timed out (sw.err): the result is reported as a NaN cost
-    const bool aborted = sw.err && *sw.err != 0;
-    if (t == 0 && sw.epoch) atomicAdd(sw.epoch, 1u);  // the next call's granule tags
     if (TAIL && seq_dev && t == HPE_NT - 64) {
         // pipelined tracking: this frame's refine launch (and the preparation of the next
         // frame inside it, which read a pinned host buffer) has completed; publish the
@@ -1060,7 +742,7 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
         out[t] = bp;
         sw.gpos[t] = bp;
     }
-    if (t == 0) out[HPE_DOF] = aborted ? __builtin_nan("") : gcost;
+    if (t == 0) out[HPE_DOF] = gcost;
     for (int c = t; c < (G + 1) * GMIN_SHARDS; c += HPE_NT) sw.gmin[(size_t)c * GMIN_STRIDE] = ~0ull;
     if (TAIL) {
         if (obs_out && t < (int)(sizeof(DevObs) / 8)) ((unsigned long long *)obs_out)[t] = obs_word;
@@ -1071,7 +753,7 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
         const Pt pre = load_pt(cv, t);
         __syncthreads();
         const double c = eval_block<EV_COST, HPE_NT>(sm, o, cv, &sm.hand, nullptr, pre);
-        if (t == 0) out[HPE_DOF] = aborted ? __builtin_nan("") : c;
+        if (t == 0) out[HPE_DOF] = c;
     }
 }
 

@@ -74,26 +74,9 @@ struct DevSwarm {
     double *gpos;             // 26               gbest position (final)
     double *trace_g;          // [G]
     int *trace_count, *trace_topo;
-    // grid-resident form (k_pso_loop): 16-B {tag, value} granules
-    struct Gran *gib;         // 2 x 2 x P x K x GR_ROW  [g&1][kept, rebuilt][receiver][slot][field]
-    struct Gran *gcell;       // 2 x P   {tag, pbest cost} per particle and generation parity
-    const uint8_t *indeg;     // (G+1) x P  in-degree of each receiver per topology
-    unsigned *epoch;          // pso_evolve call counter (bumped by k_pso_final): tags never alias
-    int *err;                 // set when a k_pso_loop wait timed out
     uint64_t seed;
     int P, G, K;
 };
-
-// One granule of the grid-resident form: written by ONE 16-B sc1 store (untorn), so a
-// reader that sees the expected tag sees the value stored with it.
-// tag = epoch << 32 | generation << 16 | sender.
-struct alignas(16) Gran {
-    unsigned long long tag;
-    double val;
-};
-#define GR_ROW 27           // granules per pushed row: pbest cost, pbest position[26]
-#define PERSIST_MAX_P 256   // particles of the grid-resident form (one workgroup per CU)
-#define PERSIST_MAX_G 4096  // generations (the receiver's in-degree column is staged in LDS)
 
 // Valid inbox slots per receiver for ONE generation g of the workgroup form, passed in the
 // kernel arguments (read with the other argument words, no dependent round trip).  Slots

@@ -444,6 +444,21 @@ void PSO::set_pso_params(arma::vec &upperbound, arma::vec &lowerbound, arma::vec
     have_params_ = true;
 }
 
+// The reference copies rows 0..12 and the three later fingers' MCP1 / MCP2 / PIP in
+// place, and writes each DIP as (2./3) * PIP with the product rounded once (PSO.cpp:169-177).
+// Out-of-range rows throw as Armadillo's bounds check does (std::logic_error).
+void PSO::dim_restore(arma::vec &theta_in, arma::vec &theta_out) {
+    if (theta_in.n_elem < 22 || theta_out.n_elem < 26)
+        throw std::logic_error("Mat::rows(): indices out of bounds or incorrectly used");
+    for (int k = 0; k <= 12; ++k) theta_out(k) = theta_in(k);  // g_rot, g_pos, thumb, index
+    theta_out(13) = 2. / 3 * theta_in(12);
+    for (int f = 0; f < 3; ++f) {  // middle, ring, little: rows 14-16, 18-20, 22-24
+        const int o = 14 + 4 * f, i = 13 + 3 * f;
+        for (int k = 0; k < 3; ++k) theta_out(o + k) = theta_in(i + k);
+        theta_out(o + 3) = 2. / 3 * theta_in(i + 2);
+    }
+}
+
 void PSO::push(hpe_ctx *c) {
     if (!have_params_) throw std::logic_error("PSO: call set_pso_params first");
     check(c, hpe_set_pso_params(c, theta_max.memptr(), theta_min.memptr(), theta_std.memptr(), w,

@@ -166,6 +166,9 @@ public:
     void set_pso_params(arma::vec &upperbound, arma::vec &lowerbound, arma::vec &std,
                         double &omega, double &phip, double &phig, int &maxiter,
                         double &minstep, double &minfunc);
+    // PSO.cpp:160-180: 22 -> 26 DOF, each finger's DIP = 2/3 of its PIP (host arithmetic;
+    // theta_out must already hold 26 elements, as the reference's .rows() assignments need)
+    void dim_restore(arma::vec &theta_in, arma::vec &theta_out);
 
     // --- extensions
     // testmodel.cpp:126-138 in one device-resident call; x0 <- bestp; returns the cost

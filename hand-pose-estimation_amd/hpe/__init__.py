@@ -363,6 +363,19 @@ class PSO:
         self.w, self.c1, self.c2 = omega, phip, phig
         self.maxiter, self.minstep, self.minfunc = maxIter, minStep, minFunc
 
+    def dim_restore(self, theta_in, theta_out):
+        """PSO.cpp:160-180: 22 -> 26 DOF in place, each finger's DIP = 2/3 of its PIP
+        (rows 13, 17, 21, 25); theta_out must hold 26 values."""
+        ti = np.asarray(theta_in, dtype=np.float64).ravel()
+        if ti.size < 22 or np.asarray(theta_out).size < 26:
+            raise IndexError("Mat::rows(): indices out of bounds or incorrectly used")
+        theta_out[0:13] = ti[0:13]
+        theta_out[13] = 2. / 3 * ti[12]
+        for f in range(3):  # middle, ring, little
+            o, i = 14 + 4 * f, 13 + 3 * f
+            theta_out[o:o + 3] = ti[i:i + 3]
+            theta_out[o + 3] = 2. / 3 * ti[i + 2]
+
     def _push(self, ctx):
         ctx.check(ctx.lib.hpe_set_pso_params(
             ctx.h, ptr(self.theta_max, C.c_double), ptr(self.theta_min, C.c_double),

@@ -15,7 +15,7 @@ PKG_DIR = Path(__file__).resolve().parent.parent  # hand-pose-estimation_amd/
 LIB_PATH = PKG_DIR / "libhpe.so"
 
 PROF_PSO_GEN, PROF_REFINE, PROF_PSO_INIT, PROF_PSO_FINAL, PROF_PREP = 0, 1, 2, 3, 4
-PROF_OPT_DESCENT, PROF_OPT_MOVE, PROF_PSO_LOOP = 5, 6, 7
+PROF_OPT_DESCENT, PROF_OPT_MOVE = 5, 6
 HPE_OK, HPE_E_ARG, HPE_E_HIP, HPE_E_STATE, HPE_E_NOMEM, HPE_E_NODEVICE = 0, -1, -2, -3, -4, -5
 
 dp = C.POINTER(C.c_double)

@@ -202,7 +202,7 @@ int hpe_track_pipelined(hpe_ctx *ctx, int num_p, int refine, double *d_state,
 #define HPE_PROF_PREP 4      /* k_preprocess (hpe_prepare_frame, preprocessing stream) */
 #define HPE_PROF_OPT_DESCENT 5 /* k_opt_descent: pso_optimise descent phase */
 #define HPE_PROF_OPT_MOVE 6    /* k_opt_move: pso_optimise velocity / cost phase */
-#define HPE_PROF_PSO_LOOP 7    /* k_pso_loop: generations 1..maxiter-1 in one grid-resident launch */
+/* 7: reserved (the grid-resident generation loop of rounds 1-2, removed) */
 #define HPE_PROF_KERNELS 8
 int hpe_profile_enable(hpe_ctx *ctx, int on);
 int hpe_profile_read(hpe_ctx *ctx, int32_t *launches, double *total_ms, double *min_ms,

@@ -1,0 +1,51 @@
+"""Config 5's multi-rank path end to end on ONE GPU: `bench.py --gpus 2 --backend gloo
+--same-device --config subswarm8` runs two ranks (one process each, both on cuda:0), each
+tracking the same frames with its own 1024-particle subswarm (seed 1000 + rank, wave form)
+through the pipelined HIP loop, and exchanging {bestp, cost} once per frame through
+hpe.dist.exchange_best (gloo through host memory here, RCCL on the 8-GPU
+node).  The state after frame 0 must equal the oracle's best of the two subswarms tracking
+that frame: refine_init_pose + pso_evolve(seed 1000 + r) + cal_cost(bestp)
+(testmodel.cpp:124-138, PSO.cpp:717-722).  Tolerances as test_gpu_configs.py."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import hand_data
+import oracle_np
+
+pytestmark = pytest.mark.gpu
+
+
+def test_bench_two_ranks_same_device_gloo(tmp_path, oracle, ora_hand):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    dump = tmp_path / "dump"
+    cmd = [sys.executable, str(hand_data.ROOT / "bench.py"), "--gpus", "2", "--backend", "gloo",
+           "--same-device", "--config", "subswarm8", "--steps", "3", "--warmup", "1",
+           "--no-cpu-baseline", "--dump", str(dump)]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["config"]["particles"] == 1024 and r["value"] > 0
+    st = [np.load(dump / f"states_rank{k}.npy") for k in range(2)]
+    assert st[0].shape == (4, 27)
+    np.testing.assert_array_equal(st[0], st[1])  # every rank adopts the same winner
+    raw0, x0 = np.load(dump / "raw0.npy"), np.load(dump / "x0.npy")
+    obs = oracle.preprocess(raw0)
+    ub, lb, sd = oracle_np.reference_bounds()
+    res = []
+    for rank in range(2):
+        xr, _ = oracle.refine(ora_hand, obs, x0)
+        xr, _, _ = oracle.pso_evolve(ora_hand, obs, xr, 1024, 31, lb, ub, sd, seed=1000 + rank)
+        res.append((oracle.cal_cost(ora_hand, obs, xr), rank, xr))
+    assert res[0][0] != res[1][0]
+    cbest, _, xbest = min(res, key=lambda e: (e[0], e[1]))
+    np.testing.assert_allclose(st[0][0, :26], xbest, rtol=0, atol=1e-6)
+    assert abs(st[0][0, 26] - cbest) <= 1e-8 * abs(cbest)

@@ -6,7 +6,11 @@ oracle on the same frames, seeds and x0.
             through pso_evolve (traces compared) and through the tracked frame
   config 3  the 400-frame sequence, 256 x 31, refine on, temporal prior, through the
             pipelined loop bench.py runs (hpe_track_pipelined, raw depth in)
-  config 4  one frame, 4096 particles x maxiter 41 in the auto (wave) form
+  config 4  one frame, 4096 particles x maxiter 41 in the auto (wave) form; and 4096 x
+            maxiter 6 at N = full (the multi-item search with the point prefetch)
+  config 3  also 20 frames at N = full (the multi-workgroup refine + fused preparation)
+  config 5  every rank's subswarm (1024 x maxiter 31, seed 1000 + r, r = 0..7) on this GPU,
+            and the best-of-8 pick over them
 
 Tolerances (as test_gpu_parity.py): pose |diff| <= 1e-6, cost relative 1e-8, gbest /
 stagnation-count / topology traces exact (gbest relative 1e-8).  Reference:
@@ -106,6 +110,117 @@ def test_config4_large_swarm_4096x40(oracle, ora_hand, gh):
     assert tr["count"].max() >= 0 and len(tr["topo"]) == 40
 
 
+def test_config4_large_swarm_full_cloud(oracle, ora_hand, gh):
+    """Config 4's swarm at N = full: 4096 particles (wave form) x maxiter 6 on a full cloud
+    (> 2048 points: every lane searches several points, the next point loaded one item
+    ahead, hpe_device.hpp search_align).  BASELINE.md §2: each config at N = 250 and full."""
+    P, maxiter = 4096, 6
+    poses = hand_data.trajectory(3, seed=45)
+    depth = gh.ctx.render_depth(poses[2])
+    obs = oracle.preprocess(depth, downsample=False)
+    assert obs.n > 2048
+    cf = _costfunc(gh, depth, False)
+    ub, lb, sd = oracle_np.reference_bounds()
+    pso = _pso(maxiter)
+    bestp = np.zeros(26)
+    assert pso.pso_evolve(cf, poses[1], P, bestp) == 1
+    rb, rc, tr = oracle.pso_evolve(ora_hand, obs, poses[1], P, maxiter, lb, ub, sd, seed=1000)
+    _check_pso(pso, cf, bestp, rb, rc, tr)
+
+
+def test_config5_subswarm_ranks_1024x30(oracle, ora_hand, gh):
+    """BASELINE config 5, one rank at a time on this GPU: rank r's subswarm is 1024
+    particles x maxiter 31 in the auto (wave, P >= 1024) form with Philox seed 1000 + r
+    (hpe.dist.subswarm_seed; the reference reseeds every call, PSO.cpp:717-722), each
+    against oracle.pso_evolve(seed=1000 + r) with traces; then hpe.dist.pick_best (the
+    per-frame exchange's choice) over the 8 GPU states picks the same rank
+    and state as over the 8 oracle states."""
+    import torch
+    from hpe.dist import pick_best, subswarm_seed
+    P, maxiter, world = 1024, 31, 8
+    poses = hand_data.trajectory(3, seed=51)
+    depth = gh.ctx.render_depth(poses[2])
+    obs = oracle.preprocess(depth)
+    cf = _costfunc(gh, depth, True)
+    ub, lb, sd = oracle_np.reference_bounds()
+    pso = _pso(maxiter)
+    hip_states, ora_states = [], []
+    for r in range(world):
+        pso.seed = subswarm_seed(r)
+        bestp = np.zeros(26)
+        assert pso.pso_evolve(cf, poses[1], P, bestp) == 1
+        rb, rc, tr = oracle.pso_evolve(ora_hand, obs, poses[1], P, maxiter, lb, ub, sd,
+                                       seed=subswarm_seed(r))
+        _check_pso(pso, cf, bestp, rb, rc, tr)
+        hip_states.append(np.concatenate([bestp, [pso.last_gbest_cost]]))
+        ora_states.append(np.concatenate([rb, [rc]]))
+    hip_states, ora_states = np.array(hip_states), np.array(ora_states)
+    assert len(set(ora_states[:, 26])) == world  # 8 distinct streams
+    hb = pick_best(torch.from_numpy(hip_states)).numpy()
+    ob = pick_best(torch.from_numpy(ora_states)).numpy()
+    assert int(np.argmin(hip_states[:, 26])) == int(np.argmin(ora_states[:, 26]))
+    np.testing.assert_allclose(hb[:26], ob[:26], rtol=0, atol=POSE_TOL)
+    assert _cost_eq(hb[26], ob[26])
+
+
+def _track_pipelined(gh, raw, P, maxiter, x0, downsample):
+    """hpe_track_pipelined over the raw frames (bench.py's loop): per-frame pose, cost and
+    the running refine evaluation count."""
+    import ctypes as C
+    import torch
+    n = len(raw)
+    ctx, lib = gh.ctx, gh.ctx.lib
+    _pso(maxiter)._push(ctx)
+    state = torch.zeros(27, dtype=torch.float64, device="cuda:0")
+    state[:26] = torch.from_numpy(np.array(x0, dtype=np.float64))
+    torch.cuda.synchronize()
+    ctx.pipeline_begin(raw[0], True, downsample)
+    gx, gc, gev = [], [], []
+    tot = C.c_uint64(0)
+    ctx.check(lib.hpe_refine_eval_count(ctx.h, C.byref(tot), 1))
+    for f in range(n):
+        ctx.track_pipelined(P, 1, state.data_ptr(), raw[f + 1] if f + 1 < n else None)
+        ctx.check(lib.hpe_sync(ctx.h))
+        torch.cuda.synchronize()
+        s = state.cpu().numpy()
+        gx.append(s[:26].copy())
+        gc.append(s[26])
+        ctx.check(lib.hpe_refine_eval_count(ctx.h, C.byref(tot), 1))
+        gev.append(tot.value)
+    gh.ctx.frame_token = None  # the pipeline owned the selected frame
+    return np.array(gx), np.array(gc), gev
+
+
+def test_config3_full_cloud_20_frames_pipelined(oracle, ora_hand, gh):
+    """Config 3's loop at N = full: 20 tracked frames, 256 x 30, refine on, through the
+    pipelined loop.  Full clouds (> 2048 points) take the multi-workgroup refine (64 helper
+    workgroups own cloud slices) with the next frame's preparation workgroups in the same
+    launch (testmodel.cpp:64 downsample = false; observedmodel.cpp:204-217 skipped).  Every
+    frame against the oracle started from the GPU's previous pose, SEQ_* tolerances."""
+    n, P, maxiter = 20, 256, 31
+    poses = hand_data.trajectory(n, seed=8, revert=0.02)
+    raw = [np.ascontiguousarray(gh.ctx.render_depth(th)) for th in poses]
+    gx, gc, gev = _track_pipelined(gh, raw, P, maxiter, poses[0], False)
+    ub, lb, sd = oracle_np.reference_bounds()
+    dpose, ev_mismatch = [], []
+    for f in range(n):
+        obs = oracle.preprocess(raw[f], downsample=False)
+        assert obs.n > 2048
+        x0 = poses[0] if f == 0 else gx[f - 1]
+        xr, er = oracle.refine(ora_hand, obs, x0)
+        xr, _, _ = oracle.pso_evolve(ora_hand, obs, xr, P, maxiter, lb, ub, sd, seed=1000)
+        cr = oracle.cal_cost(ora_hand, obs, xr)
+        dpose.append(np.abs(gx[f] - xr).max())
+        assert _cost_eq(gc[f], cr, SEQ_COST_RTOL), (f, gc[f], cr)
+        if gev[f] != er:
+            ev_mismatch.append(f)
+    dpose = np.array(dpose)
+    print(f"{n} full-cloud frames: max |dpose| {dpose.max():.3g} (frame {int(dpose.argmax())}), "
+          f"refine eval-count mismatches {len(ev_mismatch)} {ev_mismatch}")
+    assert dpose.max() <= SEQ_POSE_TOL, f"frame {int(dpose.argmax())}: pose {dpose.max()}"
+    assert len(ev_mismatch) <= max(1, n // 20)
+
+
 def test_config3_sequence_400_frames_pipelined(oracle, ora_hand, gh):
     """BASELINE config 3: 400 tracked frames, 256 x 30, refine on, x0 <- previous bestp
     (testmodel.cpp:117-139), through the pipelined loop of bench.py (raw float32 mm depth
@@ -122,31 +237,10 @@ def test_config3_sequence_400_frames_pipelined(oracle, ora_hand, gh):
     fewer and the pose moves by up to ~1e-6 (measured on this sequence: 9 of 400 frames,
     max 9.6e-7; free-running drift max 3.5e-7).  Single calls keep the
     exact eval count (test_gpu_parity.py)."""
-    import ctypes as C
-    import torch
     n, P, maxiter = 400, 256, 31
     poses = hand_data.trajectory(n, seed=7, revert=0.02)  # stays in view
     raw = [np.ascontiguousarray(gh.ctx.render_depth(th)) for th in poses]
-    ctx, lib = gh.ctx, gh.ctx.lib
-    _pso(maxiter)._push(ctx)
-    state = torch.zeros(27, dtype=torch.float64, device="cuda:0")
-    state[:26] = torch.from_numpy(poses[0].copy())
-    torch.cuda.synchronize()
-    ctx.pipeline_begin(raw[0], True, True)
-    gx, gc, gev = [], [], []
-    tot = C.c_uint64(0)
-    ctx.check(lib.hpe_refine_eval_count(ctx.h, C.byref(tot), 1))
-    for f in range(n):
-        ctx.track_pipelined(P, 1, state.data_ptr(), raw[f + 1] if f + 1 < n else None)
-        ctx.check(lib.hpe_sync(ctx.h))
-        torch.cuda.synchronize()
-        s = state.cpu().numpy()
-        gx.append(s[:26].copy())
-        gc.append(s[26])
-        ctx.check(lib.hpe_refine_eval_count(ctx.h, C.byref(tot), 1))
-        gev.append(tot.value)
-    gx, gc = np.array(gx), np.array(gc)
-    gh.ctx.frame_token = None  # the pipeline owned the selected frame
+    gx, gc, gev = _track_pipelined(gh, raw, P, maxiter, poses[0], True)
     ub, lb, sd = oracle_np.reference_bounds()
     free = poses[0].copy()
     dpose, dcost, drift, ev_mismatch = [], [], [], []

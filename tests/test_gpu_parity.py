@@ -377,58 +377,3 @@ def test_pso_evolve_block_form_inbox_counts(oracle, ora_hand, np_hand, P, maxite
     g, cnt, topo = pso.trace(cf)
     np.testing.assert_allclose(g, tr["gbest"], rtol=1e-8)
     assert np.array_equal(cnt, tr["count"]) and np.array_equal(topo, tr["topo"])
-
-
-@pytest.mark.parametrize("P,maxiter", [(256, 31), (32, 11), (7, 4), (1, 3)])
-def test_pso_evolve_grid_resident(oracle, ora_hand, np_hand, P, maxiter, monkeypatch):
-    """k_pso_loop (HPE_PSO_PERSIST=1: generations 1..maxiter-1 in one launch, generations
-    separated by data-tagged granule waits) against the oracle, twice on the same swarm
-    (the second call's granules must not match the first call's: epoch tags)."""
-    import hpe
-    monkeypatch.setenv("HPE_PSO_PERSIST", "1")
-    monkeypatch.setenv("HPE_PSO_FORM", "block")
-    gh = hpe.reference_hand(device=0)  # context created with the grid-resident form
-    truth = hand_data.trajectory(2, seed=9)[1]
-    d = oracle_np.render_depth_mm(np_hand, truth)
-    obs, om = _obs_pair(oracle, gh, d)
-    cf = hpe.costfunc(gh, om)
-    ub, lb, sd = oracle_np.reference_bounds()
-    pso = hpe.PSO()
-    pso.set_pso_params(ub, lb, sd, 0.7298, 1.49618, 1.49618, maxiter, 1e-8, 1e-8)
-    x0 = oracle_np.X0.copy()
-    rb, rc, tr = oracle.pso_evolve(ora_hand, obs, x0, P, maxiter, lb, ub, sd, seed=1000)
-    for _ in range(2):
-        bestp = np.zeros(26)
-        assert pso.pso_evolve(cf, x0, P, bestp) == 1
-        np.testing.assert_allclose(bestp, rb, rtol=0, atol=1e-6)
-        assert abs(pso.last_gbest_cost - rc) <= 1e-8 * abs(rc)
-        if maxiter > 1:
-            g, cnt, topo = pso.trace(cf)
-            np.testing.assert_allclose(g, tr["gbest"], rtol=1e-8)
-            assert np.array_equal(cnt, tr["count"]) and np.array_equal(topo, tr["topo"])
-
-
-def test_track_grid_resident_equals_launch_form(np_hand, monkeypatch):
-    """Tracked frames (refine + pso_evolve 256 x 31 + cal_cost) with the grid-resident
-    generation loop and with one launch per generation: bit-identical poses and costs."""
-    import hpe
-    poses = hand_data.trajectory(4, seed=3)
-    depths = [oracle_np.render_depth_mm(np_hand, th) for th in poses[1:]]
-    ub, lb, sd = oracle_np.reference_bounds()
-    out = {}
-    for persist in ("0", "1"):
-        monkeypatch.setenv("HPE_PSO_PERSIST", persist)
-        gh = hpe.reference_hand(device=0)
-        pso = hpe.PSO()
-        pso.set_pso_params(ub, lb, sd, 0.7298, 1.49618, 1.49618, 31, 1e-8, 1e-8)
-        x, res = poses[0].copy(), []
-        for d in depths:
-            om = hpe.observedmodel()
-            om.downsample = True
-            om.set_depth_mm(d)
-            cf = hpe.costfunc(gh, om)
-            c = pso.track_frame(cf, x, 256, refine=True)
-            res.append((x.copy(), c))
-        out[persist] = res
-    for (xa, ca), (xb, cb) in zip(out["0"], out["1"]):
-        assert np.array_equal(xa, xb) and ca == cb

@@ -120,6 +120,19 @@ def test_facade_missing_bin_aborts(facade_host):
     assert "open file for input failed" in out.stderr
 
 
+def test_dim_restore_python_mirror():
+    """PSO::dim_restore (PSO.cpp:160-180) in the Python mirror: rows copied, DIP = 2/3 PIP."""
+    import hpe
+    ti = 1.5 * np.arange(22) - 7.25
+    out = np.zeros(26)
+    hpe.PSO().dim_restore(ti, out)
+    src = list(range(13)) + [-12, 13, 14, 15, -15, 16, 17, 18, -18, 19, 20, 21, -21]
+    want = np.array([ti[k] if k >= 0 else 2. / 3 * ti[-k] for k in src])
+    assert np.array_equal(out, want)
+    with pytest.raises(IndexError):
+        hpe.PSO().dim_restore(np.zeros(20), out)
+
+
 def test_gnd_truth_err_host():
     """costfunc.cpp:476-507 restated on the host joints: zero at the true pose, and the
     six-joint sum for a known offset."""
