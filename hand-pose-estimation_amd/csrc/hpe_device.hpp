@@ -620,6 +620,93 @@ __device__ __forceinline__ unsigned sqrt_class_key(int hb, float d2) {
     return k;
 }
 
+// BFMatcher's match for the point (qx, qy, qz) over the 48 centres by a lane pair (this
+// lane: the 24 of half h), with the matched sphere's fp64 centre and radius (lanes h == 0).
+// Every lane of the wave calls it (DPP partner exchange, wave votes).
+struct BfOut {
+    int idx, ic;
+    double cx, cy, cz, cr;
+};
+__device__ __forceinline__ BfOut bf_search(const FkSm &f, const DevHand *__restrict__ H,
+                                           const float *SX, const float *SY, const float *SZ,
+                                           float qx, float qy, float qz, int h,
+                                           int g_ts = BT_GENS) {
+    typedef float f2 __attribute__((ext_vector_type(2)));  // packed fp32 (v_pk_*_f32)
+    float d2[24];
+    float m = __builtin_inff();
+    const f2 q2x = {qx, qx}, q2y = {qy, qy}, q2z = {qz, qz};
+#pragma unroll
+    for (int j = 0; j < 24; j += 2) {  // two spheres per packed op, same IEEE results
+        const f2 sx = *(const f2 *)(SX + j), sy = *(const f2 *)(SY + j),
+                 sz = *(const f2 *)(SZ + j);
+        const f2 t0 = q2x - sx, t1 = q2y - sy, t2 = q2z - sz;
+        const f2 d = (t0 * t0 + t1 * t1) + t2 * t2;
+        d2[j] = d.x;
+        d2[j + 1] = d.y;
+    }
+    {  // minimum as a three-level tree of 3-way mins (v_min3_f32), not a 12-deep chain
+        float m3[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) m3[k] = fminf(fminf(d2[3 * k], d2[3 * k + 1]), d2[3 * k + 2]);
+        m = fminf(fminf(fminf(m3[0], m3[1]), m3[2]), fminf(fminf(m3[3], m3[4]), m3[5]));
+        m = fminf(m, fminf(m3[6], m3[7]));
+    }
+    BLK_TS(g_ts, 11);
+    m = fminf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0xB1, 0xf, 0xf,
+                                                           false)));  // partner lane t^1
+    // first j with bits(d2[j]) <= hb, branch-free: key_j = j, or j | 2^31 when
+    // d2[j] > hb (non-negative floats order like their bit patterns), then an
+    // unsigned min tree and the partner lane's half
+    auto first_le = [&](int hb) {
+        unsigned key[24];
+#define HPE_KEY(J) key[J] = sqrt_class_key<J>(hb, d2[J]);
+        HPE_KEY(0) HPE_KEY(1) HPE_KEY(2) HPE_KEY(3) HPE_KEY(4) HPE_KEY(5) HPE_KEY(6) HPE_KEY(7)
+        HPE_KEY(8) HPE_KEY(9) HPE_KEY(10) HPE_KEY(11) HPE_KEY(12) HPE_KEY(13) HPE_KEY(14)
+        HPE_KEY(15) HPE_KEY(16) HPE_KEY(17) HPE_KEY(18) HPE_KEY(19) HPE_KEY(20) HPE_KEY(21)
+        HPE_KEY(22) HPE_KEY(23)
+#undef HPE_KEY
+#pragma unroll
+        for (int j = 0; j < 24; j += 3) key[j] = min(min(key[j], key[j + 1]), key[j + 2]);
+        const unsigned kx = min(min(min(key[0], key[3]), min(key[6], key[9])),
+                                min(min(key[12], key[15]), min(key[18], key[21])));
+        const int ix = (kx >= 64u) ? (1 << 20) : (int)kx + 24 * h;
+        return min(ix, __builtin_amdgcn_mov_dpp(ix, 0xB1, 0xf, 0xf, false));
+    };
+    // BFMatcher's match is the first j with d2[j] <= hi = hi_sqrt_class(m) (the sqrt
+    // class of the minimum), and hi lies within 4 ulps above m (the class of s =
+    // sqrtf(m) is narrower than 2 s ulp(s) <= 4 ulp(m)).  So the first j within 5 ulps
+    // is the match whenever its own d2 IS the minimum; only otherwise (a sphere within
+    // 5 ulps of the nearest, ahead of it: rare) is the exact class needed, by the whole
+    // wave.  The check recomputes that sphere's fp32 d2 with the search's operations.
+    int idx = first_le(__float_as_int(m) + 5);
+    // the candidate's fp64 centre and radius, read ONCE: the exact check uses the float
+    // of the centre (= Sp) and, unless the rare exact-class path moves idx, the
+    // alignment uses them as they are (one LDS round trip on the chain, not two)
+    int ic = idx < HPE_NS ? idx : 0;  // >= 48: all-NaN point (reference undefined)
+    double cx = 0, cy = 0, cz = 0, cr = 0;
+    bool exact = true;
+    if (h == 0) {
+        cx = f.S[ic][0];
+        cy = f.S[ic][1];
+        cz = f.S[ic][2];
+        cr = H->radii[ic];
+        const float tx = qx - (float)cx, ty = qy - (float)cy, tz = qz - (float)cz;
+        const float dc = (tx * tx + ty * ty) + tz * tz;
+        exact = (dc == m);  // false for NaN
+    }
+    if (__ballot(!exact)) {
+        idx = first_le(__float_as_int(hi_sqrt_class(m)));
+        ic = idx < HPE_NS ? idx : 0;
+        if (h == 0) {
+            cx = f.S[ic][0];
+            cy = f.S[ic][1];
+            cz = f.S[ic][2];
+            cr = H->radii[ic];
+        }
+    }
+    return BfOut{idx, ic, cx, cy, cz, cr};
+}
+
 // Fused correspondence search + alignment residual over NT threads.  Two lanes
 // (t, t^1) share a point, 24 spheres each; returns this thread's partial sum of
 // (|p - S[m]| - r[m])^2 and optionally stores m.
@@ -643,85 +730,15 @@ __device__ __forceinline__ double search_align(const FkSm &f, const CV &cv,
     if (gt < 0) gt = threadIdx.x;
     double acc = 0.0;
     const int h = gt & 1;
-    typedef float f2 __attribute__((ext_vector_type(2)));  // packed fp32 (v_pk_*_f32)
     const float *SX = f.Sp[0] + 24 * h, *SY = f.Sp[1] + 24 * h, *SZ = f.Sp[2] + 24 * h;
     BLK_TS(g_ts, 15);
     auto item = [&](int it, const Pt &q) {
         const int p = it >> 1;
         const double X = q.x, Y = q.y, Z = q.z;
         const float qx = (float)X, qy = (float)Y, qz = (float)Z;
-        float d2[24];
-        float m = __builtin_inff();
-        const f2 q2x = {qx, qx}, q2y = {qy, qy}, q2z = {qz, qz};
-#pragma unroll
-        for (int j = 0; j < 24; j += 2) {  // two spheres per packed op, same IEEE results
-            const f2 sx = *(const f2 *)(SX + j), sy = *(const f2 *)(SY + j),
-                     sz = *(const f2 *)(SZ + j);
-            const f2 t0 = q2x - sx, t1 = q2y - sy, t2 = q2z - sz;
-            const f2 d = (t0 * t0 + t1 * t1) + t2 * t2;
-            d2[j] = d.x;
-            d2[j + 1] = d.y;
-        }
-        {  // minimum as a three-level tree of 3-way mins (v_min3_f32), not a 12-deep chain
-            float m3[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) m3[k] = fminf(fminf(d2[3 * k], d2[3 * k + 1]), d2[3 * k + 2]);
-            m = fminf(fminf(fminf(m3[0], m3[1]), m3[2]), fminf(fminf(m3[3], m3[4]), m3[5]));
-            m = fminf(m, fminf(m3[6], m3[7]));
-        }
-        BLK_TS(g_ts, 11);
-        m = fminf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0xB1, 0xf, 0xf,
-                                                               false)));  // partner lane t^1
-        // first j with bits(d2[j]) <= hb, branch-free: key_j = j, or j | 2^31 when
-        // d2[j] > hb (non-negative floats order like their bit patterns), then an
-        // unsigned min tree and the partner lane's half
-        auto first_le = [&](int hb) {
-            unsigned key[24];
-#define HPE_KEY(J) key[J] = sqrt_class_key<J>(hb, d2[J]);
-            HPE_KEY(0) HPE_KEY(1) HPE_KEY(2) HPE_KEY(3) HPE_KEY(4) HPE_KEY(5) HPE_KEY(6) HPE_KEY(7)
-            HPE_KEY(8) HPE_KEY(9) HPE_KEY(10) HPE_KEY(11) HPE_KEY(12) HPE_KEY(13) HPE_KEY(14)
-            HPE_KEY(15) HPE_KEY(16) HPE_KEY(17) HPE_KEY(18) HPE_KEY(19) HPE_KEY(20) HPE_KEY(21)
-            HPE_KEY(22) HPE_KEY(23)
-#undef HPE_KEY
-#pragma unroll
-            for (int j = 0; j < 24; j += 3) key[j] = min(min(key[j], key[j + 1]), key[j + 2]);
-            const unsigned kx = min(min(min(key[0], key[3]), min(key[6], key[9])),
-                                    min(min(key[12], key[15]), min(key[18], key[21])));
-            const int ix = (kx >= 64u) ? (1 << 20) : (int)kx + 24 * h;
-            return min(ix, __builtin_amdgcn_mov_dpp(ix, 0xB1, 0xf, 0xf, false));
-        };
-        // BFMatcher's match is the first j with d2[j] <= hi = hi_sqrt_class(m) (the sqrt
-        // class of the minimum), and hi lies within 4 ulps above m (the class of s =
-        // sqrtf(m) is narrower than 2 s ulp(s) <= 4 ulp(m)).  So the first j within 5 ulps
-        // is the match whenever its own d2 IS the minimum; only otherwise (a sphere within
-        // 5 ulps of the nearest, ahead of it: rare) is the exact class needed, by the whole
-        // wave.  The check recomputes that sphere's fp32 d2 with the search's operations.
-        int idx = first_le(__float_as_int(m) + 5);
-        // the candidate's fp64 centre and radius, read ONCE: the exact check uses the float
-        // of the centre (= Sp) and, unless the rare exact-class path moves idx, the
-        // alignment uses them as they are (one LDS round trip on the chain, not two)
-        int ic = idx < HPE_NS ? idx : 0;  // >= 48: all-NaN point (reference undefined)
-        double cx = 0, cy = 0, cz = 0, cr = 0;
-        bool exact = true;
-        if (h == 0) {
-            cx = f.S[ic][0];
-            cy = f.S[ic][1];
-            cz = f.S[ic][2];
-            cr = H->radii[ic];
-            const float tx = qx - (float)cx, ty = qy - (float)cy, tz = qz - (float)cz;
-            const float dc = (tx * tx + ty * ty) + tz * tz;
-            exact = (dc == m);  // false for NaN
-        }
-        if (__ballot(!exact)) {
-            idx = first_le(__float_as_int(hi_sqrt_class(m)));
-            ic = idx < HPE_NS ? idx : 0;
-            if (h == 0) {
-                cx = f.S[ic][0];
-                cy = f.S[ic][1];
-                cz = f.S[ic][2];
-                cr = H->radii[ic];
-            }
-        }
+        const BfOut r = bf_search(f, H, SX, SY, SZ, qx, qy, qz, h, g_ts);
+        const int idx = r.idx, ic = r.ic;
+        const double cx = r.cx, cy = r.cy, cz = r.cz, cr = r.cr;
         if (HPE_STAMPS) asm volatile("" ::"v"(idx));
         BLK_TS(g_ts, 13);
         if (h == 0) {

@@ -528,8 +528,8 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
     const DevHand *__restrict__ H = &hs;
     FkSm &f = fks[w];
     // ---- round 1: every load of the generation, all independent and unconditional
-    Link lk[3];
-    push_lane_links(sw, g, ic, l, g + 1, -1, lk);  // var-0 links after the decision
+    // (the push links are loaded after the evaluation: held across it they would take the
+    // registers of a third wave per SIMD; the other waves hide that load)
     const CloudGlobal cv = obs_cloud(o);
     const Pt pre = load_pt(cv, l);
     const size_t e = (size_t)ic * HPE_DOF + l;
@@ -570,11 +570,6 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
     if (sg.count > 0) sg.topo = g;
     if (i == 0 && l == 0) sw.sig[g] = sg;
     const int topo = sg.topo, var = (topo == g) ? 1 : 0;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const int q = l + 64 * k;
-        if (q >= 3 * IB_FIELDS) lk[k] = load_link(sw, g, ic, q, topo);
-    }
     // ---- informant (PSO.cpp:810-812)
     const int self_lane = (K <= 15) ? 15 : 63;  // one 16-lane row when K <= 15
     double v = __builtin_inf();
@@ -625,6 +620,8 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
         sw.pb[e] = row;
         f.th[l] = row;
     }
+    Link lk[3];
+    push_lane_links(sw, g, ic, l, g + 1, topo, lk);
     if (l == 0) {
         sw.pch[(size_t)g * P + i] = pn;
         gmin_lower(sw, g, i, pn);
@@ -762,17 +759,17 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
 // as ONE persistent workgroup of RF_NT threads.  Each iteration:
 //   * f_k = cal_cost2(x0, matchId, true): FK by wave 0, search by all RF_NT threads;
 //   * the 6 central differences run concurrently, one wave each (frozen matchId);
-//   * the Goldstein bracket search is evaluated SPECULATIVELY: waves 0..2^D-2 evaluate the
-//     nodes of its next D-level decision tree (D = 3 at 8 waves, 4 at 16) (node n: down child 2n = Armijo fails,
-//     up child 2n+1 = Armijo holds but Goldstein fails), then every thread walks the
-//     tree with the serial algorithm's exact rules.  Identical arithmetic on identical
-//     alphas: the result, the step tk and the evaluation count equal the serial ones.
+//   * the Goldstein bracket search is evaluated SPECULATIVELY: each wave evaluates one node
+//     of a small tree of the search's next decisions (gold_tree, shapes below), then every
+//     thread walks the tree with the serial algorithm's exact rules.  Identical arithmetic
+//     on identical alphas: the result, the step tk and the evaluation count equal the
+//     serial ones.
 // Control flow is uniform: every thread evaluates the same scalar decisions from LDS.
 #ifndef RF_NT
 #define RF_NT 512
 #endif
 #define RF_NW (RF_NT / 64)
-#define RF_DEPTH (RF_NW >= 16 ? 4 : 3)  // speculated Goldstein levels per round
+static_assert(RF_NW >= 8, "the speculation shapes use up to 8 waves");
 #define RF_STAGE_MAX 2048  // clouds up to this size are staged in LDS with their matchId
 
 struct __align__(16) RefineSm {
@@ -992,13 +989,62 @@ __device__ void mw_helper(const DevMw &mw, int h, const DevObs *__restrict__ og,
     }
 }
 
+// Speculation shapes of the Goldstein search.  A round evaluates the nodes of a small
+// tree of decision prefixes, relative to the bracket state (a, b, alpha) at the round's
+// start: node j lies len decisions below it, decision k = bit k of bits (1 = "up": Armijo
+// holds but Goldstein fails, PSO.cpp:461-466; 0 = "down": Armijo fails, :468-471), packed
+// as byte j of nb = len << 5 | bits; nibble j of dn / up is node j's child (15: outside the
+// shape, the round ends there).  Node 0 is the current alpha.  The shape depends on the
+// previous round's last decision (context 0 = a search's first round, 1 = "down", 2 =
+// "up"): the decision logs of the bench sequence (the oracle's refine over three 40-frame
+// trajectories) are mostly runs -- "DDDDA" alone is ~27 % of the searches -- so deep runs
+// are speculated where they are likely.  Rounds over those 1,297 searches: balanced depth 3
+// (7 nodes, rounds 1-2) 3,807; the 8-node shapes 3,175; the 7-node shapes 3,361; the 4-node
+// shapes 4,553 (one node per SIMD).  The tables are compile-time constants selected by the
+// context (no memory read on the walk).  Identical arithmetic on identical alphas in every
+// shape: the walk replays the serial rules, so the result, tk and the evaluation count
+// equal the serial ones.
+struct GoldShape {
+    int n;
+    unsigned long long nb;
+    unsigned dn, up;
+};
+#define GOLD_BALANCED 0
+#define GOLD_8 1
+#define GOLD_7 2
+#define GOLD_4 3
+#ifndef HPE_GOLD_POLICY
+#define HPE_GOLD_POLICY GOLD_8  // refine_init_pose
+#endif
+template <int POL>
+__device__ __forceinline__ GoldShape gold_shape(int ctx) {
+    constexpr GoldShape T[12] = {
+    // GOLD_BALANCED
+    {7, 0x0043414240212000ull, 0xfffff531u, 0xfffff642u},  // first: '' 'D' 'U' 'DD' 'DU' 'UD' 'UU'
+    {7, 0x0043414240212000ull, 0xfffff531u, 0xfffff642u},  // D: '' 'D' 'U' 'DD' 'DU' 'UD' 'UU'
+    {7, 0x0043414240212000ull, 0xfffff531u, 0xfffff642u},  // U: '' 'D' 'U' 'DD' 'DU' 'UD' 'UU'
+    // GOLD_8
+    {8, 0xa080604340212000ull, 0xf76f5f31u, 0xfffff4f2u},  // first: '' 'D' 'U' 'DD' 'UU' 'DDD' 'DDDD' 'DDDDD'
+    {8, 0x6043414240212000ull, 0xffff7531u, 0xfffff642u},  // D: '' 'D' 'U' 'DD' 'DU' 'UD' 'UU' 'DDD'
+    {8, 0x6243414240212000ull, 0xfff7f531u, 0xfffff642u},  // U: '' 'D' 'U' 'DD' 'DU' 'UD' 'UU' 'DUD'
+    // GOLD_7
+    {7, 0x0080604340212000ull, 0xff6f5f31u, 0xfffff4f2u},  // first: '' 'D' 'U' 'DD' 'UU' 'DDD' 'DDDD'
+    {7, 0x0060414240212000ull, 0xffff6531u, 0xffffff42u},  // D: '' 'D' 'U' 'DD' 'DU' 'UD' 'DDD'
+    {7, 0x0043414240212000ull, 0xfffff531u, 0xfffff642u},  // U: '' 'D' 'U' 'DD' 'DU' 'UD' 'UU'
+    // GOLD_4
+    {4, 0x0000000043212000ull, 0xfffffff1u, 0xfffff3f2u},  // first: '' 'D' 'U' 'UU'
+    {4, 0x0000000060402000ull, 0xfffff321u, 0xffffffffu},  // D: '' 'D' 'DD' 'DDD'
+    {4, 0x0000000040212000ull, 0xffffff31u, 0xfffffff2u},  // U: '' 'D' 'U' 'DD'
+    };
+    return ctx == 0 ? T[3 * POL] : ctx == 1 ? T[3 * POL + 1] : T[3 * POL + 2];
+}
+
 // goldstein(x, g, matchId, f_k, optfunc, tk, 30) (PSO.cpp:438-480) along rs.p from rs.x0
-// with frozen correspondences, speculated RF_DEPTH levels per round: wave w evaluates tree
-// node w + 1 (root = current alpha, child 2n = "f1 > armijo" branch, 2n + 1 = "f1 <
-// goldstein" branch) and the walk replays the serial rules.  Returns tk (0 after 30
-// rejected trials); the accepted node's spheres are copied into rs.base and its cost to
-// *f_acc.  evals grows by the serial evaluation count.
-template <bool MW = false, class CV>
+// with frozen correspondences, speculated per round with shape policy POL (above): wave w
+// evaluates node w, then every thread walks the nodes with the serial algorithm's rules.
+// Returns tk (0 after 30 rejected trials); the accepted node's spheres are copied into
+// rs.base and its cost to *f_acc.  evals grows by the serial evaluation count.
+template <bool MW = false, int POL = GOLD_BALANCED, class CV>
 __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const CV &cv,
                                             const DevHand *__restrict__ H,
                                             const int32_t *__restrict__ match, double fk,
@@ -1009,47 +1055,53 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
     StampClock sc;
     sc.start();
     double A = 0, B = 1e100, alpha = 0.5, tk = 0;
-    int it = 0, accepted = -1;
+    int it = 0, accepted = -1, ctx = 0;
     bool done = false;
     [[maybe_unused]] unsigned long long path = 0;  // diagnostic build: decision bits (1 = up)
     while (!done) {
-        if (w < (1 << RF_DEPTH) - 1) {
-            const int node = w + 1, depth = 31 - __builtin_clz(node);
+        const GoldShape sh = gold_shape<POL>(ctx);
+        const int nn = sh.n;
+        if (w < nn) {
             double a = A, b = B, al2 = alpha;
-            for (int k = depth - 1; k >= 0; --k) {
-                if ((node >> k) & 1) gold_up(a, b, al2);
+            const int nbw = (int)((sh.nb >> (8 * w)) & 0xff), len = nbw >> 5, bits = nbw & 31;
+            for (int k = 0; k < len; ++k) {
+                if ((bits >> k) & 1) gold_up(a, b, al2);
                 else gold_down(a, b, al2);
             }
             if (l < HPE_DOF) rs.w[w].th[l] = rs.x0[l] + al2 * rs.p[l];
         }
-        eval_nodes<MW>(rs, (1 << RF_DEPTH) - 1, o, cv, H, match, Xt, ml, flag);
+        eval_nodes<MW>(rs, nn, o, cv, H, match, Xt, ml, flag);
         if (MW && ml->failed) break;  // the launch is ending early (DevMw::err)
-        int node = 1;
+        int node = 0;
         accepted = -1;
-        for (int lev = 0; lev < RF_DEPTH && !done; ++lev) {
+#pragma unroll
+        for (int lev = 0; lev < 6; ++lev) {  // the deepest shape path is 6 nodes
+            if (node >= 15 || done) break;
             if (it >= 30) {
                 done = true;
                 tk = 0;
                 break;
             }
             ++it;
-            const double f1 = rs.f[node - 1];
+            const double f1 = rs.f[node];
             const double armijo = fk + 0.25 * alpha * gp;
             const double gold = fk + (1 - 0.25) * alpha * gp;
             if (f1 <= armijo) {
                 if (f1 >= gold) {
                     tk = alpha;
                     done = true;
-                    accepted = node - 1;
+                    accepted = node;
                 } else {
                     gold_up(A, B, alpha);
-                    node = 2 * node + 1;
+                    node = (int)((sh.up >> (4 * node)) & 15u);
+                    ctx = 2;
                     if (HPE_STAMPS) path |= 1ull << (it - 1);
                     if (HPE_STAMPS && blockIdx.x == 0 && t == 0) hpe_stamps[8] += 1;
                 }
             } else {
                 gold_down(A, B, alpha);
-                node = 2 * node;
+                node = (int)((sh.dn >> (4 * node)) & 15u);
+                ctx = 1;
                 if (HPE_STAMPS && blockIdx.x == 0 && t == 0) hpe_stamps[7] += 1;
             }
         }
@@ -1199,7 +1251,7 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
             }
             const double gp = v1 + v2;
             // goldstein(x0, grad, matchId, f_k, optfunc, tk, 30)
-            const double tk = gold_tree<MW>(rs, o, cv, H, match, fk, gp, evals, nullptr, Xt, &ml, &mwflag);
+            const double tk = gold_tree<MW, HPE_GOLD_POLICY>(rs, o, cv, H, match, fk, gp, evals, nullptr, Xt, &ml, &mwflag);
             sc.lap(22);
             if (tk == 0) cnt += 1;
             {  // tol = sqrt(sum(grad % grad)): arrayops::accumulate over the squares
