@@ -913,25 +913,26 @@ __device__ __forceinline__ double eval_block(Smem &sm, const DevObs &o, const CV
 // the total.
 // Xt != nullptr: f.th differs from the theta of Xt only in the global position
 // (FK_TRANSLATE).
-template <bool OUTLINE_TRIG = false, class CV>
-__device__ __forceinline__ double eval_wave_frozen(FkSm &f, const DevObs &o,
-                                                   const CV &cv,
-                                                   const DevHand *__restrict__ H,
-                                                   const int32_t *__restrict__ match,
-                                                   FkX *Xt = nullptr) {
+// In two halves: frozen_head (FK, the depth gathers issued, the collision sum) needs no
+// correspondences, so the refine runs it for the gradient points while the previous
+// correspondence search is still being reduced; frozen_tail (frozen alignment, depth,
+// the three wave sums) reads matchId.
+struct FrozenHead {
+    DepthG dg;
+    double co;
+};
+template <bool OUTLINE_TRIG = false>
+__device__ __forceinline__ FrozenHead frozen_head(FkSm &f, const DevObs &o,
+                                                  const DevHand *__restrict__ H,
+                                                  FkX *Xt = nullptr) {
     if (Xt) fk_wave_t<FK_TRANSLATE>(f, H, Xt);
     else fk_wave<OUTLINE_TRIG>(f, H);
-    StampClock sc;
-    sc.start();
     const int l = threadIdx.x & 63;
-    const DepthG dg = depth_issue(f, l, o, H);
-    sc.lap(15);
-    double al = align_frozen(f, cv, H, match, l, 64);
-    sc.lap(16);
+    FrozenHead r;
+    r.dg = depth_issue(f, l, o, H);
     // three pairs per lane (the third for lanes 0..15, computed by every lane at a clamped
     // index and selected): every LDS read of the three is issued before any is used, so
-    // they share one round trip, and the sum is complete before depth_finish's wait for
-    // the gathers (the empty asm uses it; asm statements keep their order)
+    // they share one round trip
     CollPair cp[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) cp[k] = collide_load(f, k < 2 ? l + 64 * k : ((l < 16) ? l + 128 : l), H);
@@ -946,14 +947,30 @@ __device__ __forceinline__ double eval_wave_frozen(FkSm &f, const DevObs &o,
 #pragma unroll
         for (int k = 0; k < 3; ++k) rt[k] = hpe_sqrt_direct(d2[k]) ? rt[k] : sqrt(d2[k]);
     }
-    double co = collide_value(cp[0], rt[0]) + collide_value(cp[1], rt[1]) +
-                ((l < 16) ? collide_value(cp[2], rt[2]) : 0.0);
-    asm volatile("" ::"v"(co));
-    double dep = depth_finish(dg, o, l < HPE_NS);
-    sc.lap(17);
+    r.co = collide_value(cp[0], rt[0]) + collide_value(cp[1], rt[1]) +
+           ((l < 16) ? collide_value(cp[2], rt[2]) : 0.0);
+    return r;
+}
+template <class CV>
+__device__ __forceinline__ double frozen_tail(const FkSm &f, const DevObs &o, const CV &cv,
+                                              const DevHand *__restrict__ H,
+                                              const int32_t *__restrict__ match,
+                                              FrozenHead hd) {
+    const int l = threadIdx.x & 63;
+    double al = align_frozen(f, cv, H, match, l, 64);
+    double co = hd.co;
+    asm volatile("" ::"v"(co));  // complete before depth_finish's wait for the gathers
+    double dep = depth_finish(hd.dg, o, l < HPE_NS);
     wave_sum3(al, dep, co);
-    sc.lap(18);
     return (al * o.lambda + dep) + co;
+}
+template <bool OUTLINE_TRIG = false, class CV>
+__device__ __forceinline__ double eval_wave_frozen(FkSm &f, const DevObs &o,
+                                                   const CV &cv,
+                                                   const DevHand *__restrict__ H,
+                                                   const int32_t *__restrict__ match,
+                                                   FkX *Xt = nullptr) {
+    return frozen_tail(f, o, cv, H, match, frozen_head<OUTLINE_TRIG>(f, o, H, Xt));
 }
 
 // ---------------------------------------------------------------- Philox4x32-10

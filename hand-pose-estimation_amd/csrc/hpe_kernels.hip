@@ -1222,17 +1222,62 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
                 __syncthreads();
             }
             REF_TS(rs.ts_n, 1);
-            const double fk = eval_corr<MW>(rs, o, cv, H, match, &ml, &mwflag);
-            ++evals;
-            REF_TS(rs.ts_n, 2);
-            sc.lap(20);
-            // cal_grad: x0 +/- e along the 3 block dims, one wave per evaluation
-            if (w < 6) {
-                const int d = lo + (w >> 1);
-                if (l < HPE_DOF)
-                    rs.w[w].th[l] = (l == d) ? ((w & 1) ? rs.x0[l] - e : rs.x0[l] + e) : rs.x0[l];
+            double fk;
+            if (MW) {
+                fk = eval_corr<MW>(rs, o, cv, H, match, &ml, &mwflag);
+                REF_TS(rs.ts_n, 2);
+                // cal_grad: x0 +/- e along the 3 block dims, one wave per evaluation
+                if (w < 6) {
+                    const int d = lo + (w >> 1);
+                    if (l < HPE_DOF)
+                        rs.w[w].th[l] = (l == d) ? ((w & 1) ? rs.x0[l] - e : rs.x0[l] + e) : rs.x0[l];
+                }
+                eval_nodes<MW>(rs, 6, o, cv, H, match, Xt, &ml, &mwflag);
+            } else {
+                // f_k = cal_cost2(x0, matchId, true) and cal_grad's six frozen evaluations
+                // (x0 +/- e along the 3 block dims, one wave each) with one barrier between
+                // them: the search stores matchId, and while the slowest search waves and the
+                // corr sums finish, waves 0..5 already run the parts of their gradient point
+                // that need no matchId (FK, depth gathers, collision)
+                const DepthG dgc = depth_issue_w0(rs.base, o, H);
+                const bool young = w >= HPE_SETPRIO_FROM;  // as in eval_block
+                if (young) __builtin_amdgcn_s_setprio(1);
+                double al = search_align<RF_NT, true>(rs.base, cv, H, match, load_pt(cv, t));
+                if (young) __builtin_amdgcn_s_setprio(0);
+                double co = (t < 144) ? collide_term(rs.base, t, H) : 0.0;
+                double dep = depth_finish(dgc, o, t < HPE_NS);
+                wave_sum3(al, dep, co);  // the corr sums, as block_sum3 orders them
+                if (l == 0) {
+                    rs.red[w][0] = al;
+                    rs.red[w][1] = dep;
+                    rs.red[w][2] = co;
+                }
+                FrozenHead hd{};
+                if (w < 6) {
+                    const int d = lo + (w >> 1);
+                    if (l < HPE_DOF)
+                        rs.w[w].th[l] = (l == d) ? ((w & 1) ? rs.x0[l] - e : rs.x0[l] + e) : rs.x0[l];
+                    wave_sync();
+                    hd = frozen_head<true>(rs.w[w], o, H, Xt);
+                }
+                __syncthreads();  // matchId complete, the corr partial sums in red
+                double ra = 0, rb = 0, rc = 0;
+#pragma unroll
+                for (int k = 0; k < RF_NW; ++k) {
+                    ra += rs.red[k][0];
+                    rb += rs.red[k][1];
+                    rc += rs.red[k][2];
+                }
+                fk = (ra * o.lambda + rb) + rc;
+                REF_TS(rs.ts_n, 2);
+                if (w < 6) {
+                    const double f = frozen_tail(rs.w[w], o, cv, H, match, hd);
+                    if (l == 0) rs.f[w] = f;
+                }
+                __syncthreads();
             }
-            eval_nodes<MW>(rs, 6, o, cv, H, match, Xt, &ml, &mwflag);
+            ++evals;
+            sc.lap(20);
             evals += 6;
             if (t < HPE_DOF) {
                 const double g = (t >= lo && t <= hi)
@@ -1244,24 +1289,21 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
             __syncthreads();
             REF_TS(rs.ts_n, 3);
             sc.lap(21);
-            double v1 = 0, v2 = 0;  // op_dot::direct_dot_arma (two accumulators)
-            for (int a = 0, b = 1; b < HPE_DOF; a += 2, b += 2) {
-                v1 += rs.g[a] * rs.p[a];
-                v2 += rs.g[b] * rs.p[b];
-            }
-            const double gp = v1 + v2;
+            // g'p by op_dot::direct_dot_arma (two accumulators: even / odd indices).  g is
+            // zero outside the block, and a zero term leaves an accumulator unchanged
+            // (x + -0 = x; the empty sums stay zero), so the sums reduce to the block's
+            // terms in the same order: block 0 (dims 0..2) v1 = g0 p0 + g2 p2, v2 = g1 p1;
+            // block 1 (dims 3..5) v1 = g4 p4, v2 = g3 p3 + g5 p5.  Same for |g|^2 (tol).
+            const double g0 = rs.g[lo], g1 = rs.g[lo + 1], g2 = rs.g[lo + 2];
+            const double q0 = g0 * (-1 * g0), q1 = g1 * (-1 * g1), q2 = g2 * (-1 * g2);
+            const double s0 = g0 * g0, s1 = g1 * g1, s2 = g2 * g2;
+            const double gp = (blk == 0) ? (q0 + q2) + q1 : q1 + (q0 + q2);
             // goldstein(x0, grad, matchId, f_k, optfunc, tk, 30)
             const double tk = gold_tree<MW, HPE_GOLD_POLICY>(rs, o, cv, H, match, fk, gp, evals, nullptr, Xt, &ml, &mwflag);
             sc.lap(22);
             if (tk == 0) cnt += 1;
-            {  // tol = sqrt(sum(grad % grad)): arrayops::accumulate over the squares
-                double a1 = 0, a2 = 0;
-                for (int a = 0, b = 1; b < HPE_DOF; a += 2, b += 2) {
-                    a1 += rs.g[a] * rs.g[a];
-                    a2 += rs.g[b] * rs.g[b];
-                }
-                tol = sqrt(a1 + a2);
-            }
+            // tol = sqrt(sum(grad % grad)): arrayops::accumulate (two accumulators)
+            tol = sqrt((blk == 0) ? (s0 + s2) + s1 : s1 + (s0 + s2));
             iter += 1;
             __syncthreads();
             if (t < HPE_DOF) rs.x0[t] = rs.x0[t] - tk * rs.g[t];

@@ -23,7 +23,7 @@ P = int(sys.argv[2]) if len(sys.argv) > 2 else 256
 GENS, BLK, PTS = 48, 256, 24
 hand = hpe.reference_hand()
 ctx = hand.ctx
-poses = synth.trajectory(nfr + 1, 0)
+poses = synth.trajectory(nfr + 1, 0, revert=0.02)  # the bench sequence
 raw = [np.ascontiguousarray(ctx.render_depth(th)) for th in poses]
 ub, lb, sd = hpe.reference_bounds()
 ctx.check(lib.hpe_set_pso_params(ctx.h, _lib.ptr(ub, C.c_double), _lib.ptr(lb, C.c_double),
