@@ -1193,7 +1193,7 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
     bool base_valid = false;
     const double e = 1e-5;  // cal_grad step (PSO.cpp:195)
     for (int blk = 0; blk < 2; ++blk) {
-        const int lo = 3 * blk, hi = 3 * blk + 2;  // start_idx/end_idx (PSO.cpp:226-227)
+        const int lo = 3 * blk;  // start_idx (PSO.cpp:226-227); end_idx = lo + 2
         // Block 2 moves only the global position u = x0[3..5]: every FK of the block is
         // the stored rotation terms of x0 plus u (FK_TRANSLATE, bit-identical).
         FkX *Xt = nullptr;
@@ -1279,8 +1279,8 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
             ++evals;
             sc.lap(20);
             evals += 6;
-            if (t < HPE_DOF) {
-                const double g = (t >= lo && t <= hi)
+            if (t < HPE_DOF) {  // PSO.cpp:197-212; p = -1 * grad
+                const double g = (t >= lo && t <= lo + 2)
                                      ? (rs.f[2 * (t - lo)] - rs.f[2 * (t - lo) + 1]) / (2 * e)
                                      : 0.0;
                 rs.g[t] = g;
@@ -1305,7 +1305,7 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
             // tol = sqrt(sum(grad % grad)): arrayops::accumulate (two accumulators)
             tol = sqrt((blk == 0) ? (s0 + s2) + s1 : s1 + (s0 + s2));
             iter += 1;
-            __syncthreads();
+            // (gold_tree ended with a barrier: every read of x0 in it is done)
             if (t < HPE_DOF) rs.x0[t] = rs.x0[t] - tk * rs.g[t];
             base_valid = true;  // accepted node copied, or tk == 0 and x0 unchanged
             __syncthreads();

@@ -150,23 +150,17 @@ __global__ __launch_bounds__(RF_NT) void k_opt_descent(DevOpt op, const DevObs *
         }
         __syncthreads();
         const double gs = (rs.f[0] - rs.f[1]) / (2 * e5);
-        if (t < HPE_DOF) {
-            const double gv = (t == sel) ? gs : 0.0;
-            rs.g[t] = gv;
-            rs.p[t] = -1 * gv;
-        }
-        __syncthreads();
-        double v1 = 0, v2 = 0;  // dot(g, p): two accumulators (op_dot::direct_dot_arma)
-        for (int a = 0, b = 1; b < HPE_DOF; a += 2, b += 2) {
-            v1 += rs.g[a] * rs.p[a];
-            v2 += rs.g[b] * rs.p[b];
-        }
-        const double gp = v1 + v2;
+        // g is gs on coordinate sel, 0 elsewhere, p = -1 * g; dot(g, p) by two accumulators
+        // (op_dot::direct_dot_arma) has the one nonzero term, exactly
+        const double gl = (t == sel) ? gs : 0.0;
+        const double gp = gs * (-1 * gs);
+        if (t < HPE_DOF) rs.p[t] = -1 * gl;
+        __syncthreads();  // p published; rs.f is the Goldstein nodes' next
         sc.lap(27);
         double facc = fk;
         const double tk = gold_tree(rs, o, cv, H, match, fk, gp, evals, &facc);
         sc.start();
-        if (t < HPE_DOF) rs.x0[t] = rs.x0[t] - tk * rs.g[t];
+        if (t < HPE_DOF) rs.x0[t] = rs.x0[t] - tk * gl;
         __syncthreads();
         double f2 = fk;  // tk == 0: theta unchanged, same matchId -> same cost
         if (tk != 0) {
