@@ -239,8 +239,15 @@ __device__ __noinline__ SinCos sincos_outline(double a) {
     return r;
 }
 
+// A sphere centre as FK stores it (y and z negated): lane l < 48 gets sphere l's
+// coordinates in registers, so its depth projection needs no LDS round trip.
+struct SphXYZ {
+    double x, y, z;
+};
+
 template <int MODE, bool OUTLINE_TRIG = false>
-__device__ __forceinline__ void fk_wave_t(FkSm &f, const DevHand *__restrict__ H, FkX *X) {
+__device__ __forceinline__ void fk_wave_t(FkSm &f, const DevHand *__restrict__ H, FkX *X,
+                                          SphXYZ *own = nullptr) {
     const int l = threadIdx.x & 63;
     StampClock sc;
     sc.start();
@@ -251,16 +258,9 @@ __device__ __forceinline__ void fk_wave_t(FkSm &f, const DevHand *__restrict__ H
     const double Fc = H->Fc[dl], Fs = H->Fs[dl], FLc = H->FLc[dl], FLs = H->FLs[dl];
     const double T10x = H->T10x[dl], T10y = H->T10y[dl];
     const double L1 = H->L[dl][1], tc = H->twc[dl], ts = H->tws[dl];
-    int sd[3], sa[3];
-    double swa[3], swb[3];
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-        const int it = l + 64 * q, s = (it < 3 * HPE_NS) ? it / 3 : 0;
-        sd[q] = H->dg[s];
-        sa[q] = H->ja[s];
-        swa[q] = H->wa[s];
-        swb[q] = H->wb[s];
-    }
+    const int sl = (l < HPE_NS) ? l : HPE_NS - 1;  // this lane's sphere
+    const int sd = H->dg[sl], sa = H->ja[sl];
+    const double swa = H->wa[sl], swb = H->wb[sl];
     if (MODE != FK_TRANSLATE) {
         if (l < 23) {
             // one unconditional LDS read per lane (per-lane branches would serialise three
@@ -354,35 +354,39 @@ __device__ __forceinline__ void fk_wave_t(FkSm &f, const DevHand *__restrict__ H
         f.J[d][4][r] = J4;
     }
     wave_sync();
-    // spheres (fingermodel.cpp:208-267, thumbmodel.cpp:227-274): 144 (sphere, coord)
-    // items over the wave, weights from the hand tables; cols(1,2) *= -1 (handmodel.cpp:288).
-    // Every item's joint reads are issued first (unconditional; the third item of lanes
-    // >= 16 reads a valid clamped entry), so the three items share one LDS round trip.
+    // spheres (fingermodel.cpp:208-267, thumbmodel.cpp:227-274): lane l < 48 places sphere
+    // l, its three coordinates, weights from the hand tables; cols(1,2) *= -1
+    // (handmodel.cpp:288).  Its six joint reads are issued first (unconditional: lanes >= 48
+    // read sphere 47's), so they share one LDS round trip; the centre stays in the lane's
+    // registers for the caller's depth projection (own).
     double ja[3], jb[3];
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-        const int it = l + 64 * q, r = (it < 3 * HPE_NS) ? it - 3 * (it / 3) : 0;
-        ja[q] = f.J[sd[q]][sa[q]][r];
-        jb[q] = f.J[sd[q]][sa[q] + 1][r];
+    for (int r = 0; r < 3; ++r) {
+        ja[r] = f.J[sd][sa][r];
+        jb[r] = f.J[sd][sa + 1][r];
     }
+    double vs[3];
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-        const int it = l + 64 * q;
-        if (it < 3 * HPE_NS) {
-            const int s = it / 3, r = it - 3 * (it / 3);
-            const double v = swa[q] * ja[q] + swb[q] * jb[q];
-            const double vs = (r == 0) ? v : v * -1;
-            f.S[s][r] = vs;
-            f.Sp[r][s] = (float)vs;
+    for (int r = 0; r < 3; ++r) {
+        const double v = swa * ja[r] + swb * jb[r];
+        vs[r] = (r == 0) ? v : v * -1;
+    }
+    if (l < HPE_NS) {
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            f.S[l][r] = vs[r];
+            f.Sp[r][l] = (float)vs[r];
         }
     }
+    if (own) *own = (l < HPE_NS) ? SphXYZ{vs[0], vs[1], vs[2]} : SphXYZ{0.0, 0.0, 0.0};
     wave_sync();
     sc.lap(14);
 }
 
 template <bool OUTLINE_TRIG = false>
-__device__ __forceinline__ void fk_wave(FkSm &f, const DevHand *__restrict__ H) {
-    fk_wave_t<FK_FULL, OUTLINE_TRIG>(f, H, nullptr);
+__device__ __forceinline__ void fk_wave(FkSm &f, const DevHand *__restrict__ H,
+                                        SphXYZ *own = nullptr) {
+    fk_wave_t<FK_FULL, OUTLINE_TRIG>(f, H, nullptr, own);
 }
 
 // ---------------------------------------------------------------- reductions
@@ -520,10 +524,10 @@ struct DepthG {
     float dtp;
     bool in;
 };
-__device__ __forceinline__ DepthG depth_issue(const FkSm &f, int i, const DevObs &o,
-                                              const DevHand *__restrict__ H) {
+__device__ __forceinline__ DepthG depth_issue_at(const SphXYZ &c, int i, const DevObs &o,
+                                                 const DevHand *__restrict__ H) {
     i = i < HPE_NS ? i : HPE_NS - 1;
-    const double x = f.S[i][0], y = f.S[i][1] * -1, z = f.S[i][2] * -1;
+    const double x = c.x, y = c.y * -1, z = c.z * -1;
     const double pu = (o.K[0] * x + o.K[1] * y) + o.K[2] * z;
     const double pv = (o.K[3] * x + o.K[4] * y) + o.K[5] * z;
     const double pw = (o.K[6] * x + o.K[7] * y) + o.K[8] * z;
@@ -541,6 +545,11 @@ __device__ __forceinline__ DepthG depth_issue(const FkSm &f, int i, const DevObs
     d.z = z;
     d.r = H->radii[i];
     return d;
+}
+__device__ __forceinline__ DepthG depth_issue(const FkSm &f, int i, const DevObs &o,
+                                              const DevHand *__restrict__ H) {
+    const int ic = i < HPE_NS ? i : HPE_NS - 1;
+    return depth_issue_at(SphXYZ{f.S[ic][0], f.S[ic][1], f.S[ic][2]}, i, o, H);
 }
 __device__ __forceinline__ double depth_finish(DepthG d, const DevObs &o, bool use) {
     asm volatile("" : "+v"(d.djc), "+v"(d.dtp));
@@ -845,8 +854,9 @@ template <class CV>
 __device__ __forceinline__ double eval_wave_cost(FkSm &f, const DevObs &o, const CV &cv,
                                                  const DevHand *__restrict__ H, Pt pre) {
     const int l = threadIdx.x & 63;
-    fk_wave(f, H);
-    const DepthG dg = depth_issue(f, l, o, H);
+    SphXYZ own;
+    fk_wave(f, H, &own);
+    const DepthG dg = depth_issue_at(own, l, o, H);
     double al = search_align<64, false>(f, cv, H, nullptr, pre, l);
     double dep = depth_finish(dg, o, l < HPE_NS);
     double co = 0.0;
@@ -862,21 +872,31 @@ __device__ __forceinline__ CloudGlobal obs_cloud(const DevObs &o) {
 // search).  Every thread returns the total; terms (align, depth, collision) go to
 // sm.dscal[0..2].
 // FK = false: the caller has already placed the centres in sm.fk.S / Sp (hpe_eval_spheres).
+// dg_w0 (FK = false): wave 0's depth gathers, already issued by the caller right after its
+// FK (depth_issue_at on the centres FK left in registers); otherwise they are issued here.
 template <int MODE, int NT, bool FK = true, class CV>
 __device__ __forceinline__ double eval_block(Smem &sm, const DevObs &o, const CV &cv,
                                              const DevHand *__restrict__ H,
                                              int32_t *__restrict__ match, Pt pre,
-                                             int g_ts = BT_GENS) {
+                                             int g_ts = BT_GENS, const DepthG *dg_w0 = nullptr) {
     StampClock sc;
     sc.start();
+    const int t = threadIdx.x;
+    DepthG dg{0.0, 0.0, 0.0, 0.f, false};
     if (FK) {
-        if (threadIdx.x < 64) fk_wave(sm.fk, H);
+        if (t < 64) {
+            SphXYZ own;
+            fk_wave(sm.fk, H, &own);
+            dg = depth_issue_at(own, t, o, H);  // issued before the barrier
+        }
         __syncthreads();
+    } else if (dg_w0) {
+        dg = *dg_w0;
+    } else {
+        // issue the depth gathers first: their latency hides under the search
+        dg = depth_issue_w0(sm.fk, o, H);
     }
     sc.lap(10);
-    const int t = threadIdx.x;
-    // issue the depth gathers first: their latency hides under the search
-    const DepthG dg = depth_issue_w0(sm.fk, o, H);
     // Waves 4..7 share the SIMDs with waves 0..3 and lose the age arbitration: they reached
     // the reduction ~0.5 us after waves 1..3.  Static priority for that half during the
     // search (MI355X_MICROARCH.md, two waves per SIMD, item 4).
@@ -925,11 +945,12 @@ template <bool OUTLINE_TRIG = false>
 __device__ __forceinline__ FrozenHead frozen_head(FkSm &f, const DevObs &o,
                                                   const DevHand *__restrict__ H,
                                                   FkX *Xt = nullptr) {
-    if (Xt) fk_wave_t<FK_TRANSLATE>(f, H, Xt);
-    else fk_wave<OUTLINE_TRIG>(f, H);
+    SphXYZ own;
+    if (Xt) fk_wave_t<FK_TRANSLATE>(f, H, Xt, &own);
+    else fk_wave<OUTLINE_TRIG>(f, H, &own);
     const int l = threadIdx.x & 63;
     FrozenHead r;
-    r.dg = depth_issue(f, l, o, H);
+    r.dg = depth_issue_at(own, l, o, H);
     // three pairs per lane (the third for lanes 0..15, computed by every lane at a clamped
     // index and selected): every LDS read of the three is issued before any is used, so
     // they share one round trip

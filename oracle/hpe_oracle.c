@@ -558,10 +558,30 @@ int ora_pso_evolve(const ora_hand *h, const ora_obs *o, const double x0[26], int
     return 1;
 }
 
+/* Diagnostic decision log of the Goldstein searches (tools/gold_shapes.py, the input for
+ * the GPU's speculation shapes): per search, decision bits (1 = up) | trials << 32 |
+ * accepted << 40.  Off unless ora_set_gold_log sets a buffer. */
+static uint64_t *g_gold_log = NULL;
+static int g_gold_cap = 0, g_gold_n = 0;
+void ora_set_gold_log(uint64_t *buf, int cap) {
+    g_gold_log = buf;
+    g_gold_cap = cap;
+    g_gold_n = 0;
+}
+int ora_gold_log_count(void) { return g_gold_n; }
+static void gold_log(uint64_t path, int trials, int accepted) {
+    if (!g_gold_log) return;
+    int k;
+#pragma omp atomic capture
+    k = g_gold_n++;
+    if (k < g_gold_cap) g_gold_log[k] = path | ((uint64_t)trials << 32) | ((uint64_t)accepted << 40);
+}
+
 /* goldstein, PSO.cpp:438-480 */
 static double goldstein(const ora_hand *h, const ora_obs *o, const double *theta,
                         const double *g, int32_t *match, double fk, int maxiter, int *evals) {
     double a = 0, b = 1e100, alpha = 0.5;
+    uint64_t path = 0;
     const double t = 2, c = 0.25;
     double p[26], th1[26];
     for (int d = 0; d < 26; ++d) p[d] = -1 * g[d];
@@ -573,15 +593,20 @@ static double goldstein(const ora_hand *h, const ora_obs *o, const double *theta
         const double armijo = fk + c * alpha * gp;
         const double gold = fk + (1 - c) * alpha * gp;
         if (f1 <= armijo) {
-            if (f1 >= gold) return alpha;
+            if (f1 >= gold) {
+                gold_log(path, it + 1, 1);
+                return alpha;
+            }
             a = alpha;
             const double up = t * alpha, mid = 0.5 * (alpha + b);
             alpha = (mid < up) ? mid : up; /* std::min */
+            path |= 1ull << it;
         } else {
             b = alpha;
             alpha = 0.5 * (a + alpha);
         }
     }
+    gold_log(path, maxiter, 0);
     return 0;
 }
 

@@ -88,6 +88,9 @@ int ora_pso_evolve(const ora_hand *h, const ora_obs *o, const double x0[26], int
                    double *bestcost, ora_pso_trace *trace, int nthreads);
 
 int ora_refine_init_pose(const ora_hand *h, const ora_obs *o, double x0[26]);
+/* diagnostic: log every Goldstein search's decisions into buf (see hpe_oracle.c) */
+void ora_set_gold_log(uint64_t *buf, int cap);
+int ora_gold_log_count(void);
 
 int ora_pso_optimise(const ora_hand *h, const ora_obs *o, const double x0[26], int P,
                      int maxiter, const double lb[26], const double ub[26],

@@ -1,4 +1,14 @@
-// CPU emulation of the fp32 filter search vs the exact BFMatcher rule (same fp32 ops).
+// tools/experiments/filter_check.c -- CPU replay of the fp32 filter search of
+// search_filter.patch (round 3, measured slower and not kept) against the exact BFMatcher
+// rule of hpe_device.hpp (same fp32 operations, -ffp-contract=off, explicit fmaf): for
+// every (particle, cloud point) pair it reports how often the filter is not unique (the
+// exact path runs) and counts wrong answers (must be 0 at any KE; KE scales the error bound
+// E = KE u (Q + S2), the product uses 64).  Input: the binary file written by a few lines
+// of numpy (int P, int N, P x 144 doubles of sphere centres, N x 3 doubles of cloud).
+// Build: gcc -O2 -ffp-contract=off -o filter_check filter_check.c -lm
+// Run:   ./filter_check data.bin [centre sphere index = 20] [KE = 64]
+// Measured on three bench frames (100k-383k pairs): 0.12-0.16 % non-unique at KE = 64,
+// 0 wrong at KE = 64 ... 0.
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
