@@ -872,31 +872,28 @@ __device__ __forceinline__ CloudGlobal obs_cloud(const DevObs &o) {
 // search).  Every thread returns the total; terms (align, depth, collision) go to
 // sm.dscal[0..2].
 // FK = false: the caller has already placed the centres in sm.fk.S / Sp (hpe_eval_spheres).
-// dg_w0 (FK = false): wave 0's depth gathers, already issued by the caller right after its
-// FK (depth_issue_at on the centres FK left in registers); otherwise they are issued here.
+// own_w0 (FK = false): the centres wave 0's FK (run by the caller) left in its registers,
+// projected here without re-reading them from LDS; otherwise read from sm.fk.
 template <int MODE, int NT, bool FK = true, class CV>
 __device__ __forceinline__ double eval_block(Smem &sm, const DevObs &o, const CV &cv,
                                              const DevHand *__restrict__ H,
                                              int32_t *__restrict__ match, Pt pre,
-                                             int g_ts = BT_GENS, const DepthG *dg_w0 = nullptr) {
+                                             int g_ts = BT_GENS, const SphXYZ *own_w0 = nullptr) {
     StampClock sc;
     sc.start();
     const int t = threadIdx.x;
-    DepthG dg{0.0, 0.0, 0.0, 0.f, false};
+    SphXYZ own{0.0, 0.0, 0.0};
     if (FK) {
-        if (t < 64) {
-            SphXYZ own;
-            fk_wave(sm.fk, H, &own);
-            dg = depth_issue_at(own, t, o, H);  // issued before the barrier
-        }
+        if (t < 64) fk_wave(sm.fk, H, &own);
         __syncthreads();
-    } else if (dg_w0) {
-        dg = *dg_w0;
-    } else {
-        // issue the depth gathers first: their latency hides under the search
-        dg = depth_issue_w0(sm.fk, o, H);
+    } else if (own_w0) {
+        own = *own_w0;
     }
     sc.lap(10);
+    // wave 0 issues the depth gathers first (after the barrier: the other waves start
+    // searching at once): their latency hides under the search
+    DepthG dg{0.0, 0.0, 0.0, 0.f, false};
+    if (t < 64) dg = (FK || own_w0) ? depth_issue_at(own, t, o, H) : depth_issue(sm.fk, t, o, H);
     // Waves 4..7 share the SIMDs with waves 0..3 and lose the age arbitration: they reached
     // the reduction ~0.5 us after waves 1..3.  Static priority for that half during the
     // search (MI355X_MICROARCH.md, two waves per SIMD, item 4).

@@ -377,7 +377,7 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
     hand_put<HPE_NT>(sm.hand, hw);
     BLK_TS(g, 1);
     __syncthreads();  // informant rows and draws in LDS
-    DepthG dg0{0.0, 0.0, 0.0, 0.f, false};
+    SphXYZ own0{0.0, 0.0, 0.0};  // wave 0: the centres FK leaves in registers
     BLK_TS(g, 2);
     if (t < 64) {
         // ---- velocity, position, check_constraints (PSO.cpp:824-842, 358-377)
@@ -402,9 +402,7 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
         wave_sync();
         BLK_TS(g, 10);
         sc.lap(2);
-        SphXYZ own;
-        fk_wave(sm.fk, H, &own);
-        dg0 = depth_issue_at(own, t, o, H);  // wave 0's depth gathers, before the barrier
+        fk_wave(sm.fk, H, &own0);
     }
     __syncthreads();  // spheres, topology and own pbest cost published
     BLK_TS(g, 3);
@@ -412,7 +410,7 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
     const double pci = sm.dscal[4];
     const Link lk0 = load_link(sw, g, i, q, topo, q >= 3 * IB_FIELDS);
     // ---- evaluation and pbest (PSO.cpp:848-861)
-    const double fx = eval_block<EV_COST, HPE_NT, false>(sm, o, cv, H, nullptr, pre, g, &dg0);
+    const double fx = eval_block<EV_COST, HPE_NT, false>(sm, o, cv, H, nullptr, pre, g, &own0);
     BLK_TS(g, 4);
     sc.start();
     const bool better = fx < pci;
@@ -1019,9 +1017,6 @@ struct GoldShape {
 #ifndef HPE_GOLD_POLICY
 #define HPE_GOLD_POLICY GOLD_8  // refine_init_pose
 #endif
-#ifndef HPE_WALK_PREFETCH
-#define HPE_WALK_PREFETCH 1
-#endif
 template <int POL>
 __device__ __forceinline__ GoldShape gold_shape(int ctx) {
     constexpr GoldShape T[12] = {
@@ -1080,13 +1075,6 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
         if (MW && ml->failed) break;  // the launch is ending early (DevMw::err)
         int node = 0;
         accepted = -1;
-#if HPE_WALK_PREFETCH
-        // all node costs in one batch of LDS reads (a register select per level, not one
-        // dependent LDS round trip per level)
-        double fv[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) fv[k] = rs.f[k];
-#endif
 #pragma unroll
         for (int lev = 0; lev < 6; ++lev) {  // the deepest shape path is 6 nodes
             if (node >= 15 || done) break;
@@ -1096,13 +1084,7 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
                 break;
             }
             ++it;
-#if HPE_WALK_PREFETCH
-            double f1 = fv[0];
-#pragma unroll
-            for (int k = 1; k < 8; ++k) f1 = (node == k) ? fv[k] : f1;
-#else
             const double f1 = rs.f[node];
-#endif
             const double armijo = fk + 0.25 * alpha * gp;
             const double gold = fk + (1 - 0.25) * alpha * gp;
             if (f1 <= armijo) {

@@ -45,8 +45,8 @@ def decision_logs(mode, frames, seed):
             x, _ = o.refine(h, obs, x)
             x, _, _ = o.pso_evolve(h, obs, x, 256, 31, lb, ub, sd, seed=1000)
         else:
-            x, _, _ = o.pso_optimise(h, obs, x, 32, 8, lb, ub, sd, 0.7298, 1.49618, 1.49618,
-                                     seed=1000, nthreads=1)
+            x, _, _ = o.pso_optimise(h, obs, x, 32, 6, lb, ub, sd, 0.7298, 1.49618, 1.49618,
+                                     seed=1000)
     n = min(o.lib.ora_gold_log_count(), cap)
     o.lib.ora_set_gold_log(C.POINTER(C.c_uint64)(), 0)
     out = []
