@@ -635,6 +635,35 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
     }
 }
 
+// u64 wave helpers of k_pso_final's replay: lane l - 1's value (lane 0: fill), the
+// inclusive prefix minimum over lanes 0..l (DPP row_shr 1/2/4/8, row_bcast 15/31; lanes
+// without a source keep the identity, all ones), a lane's value in every lane.
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ unsigned long long dpp_min_src_u64(unsigned long long v) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(-1, (int)(unsigned)v, CTRL, ROWMASK, 0xf, false);
+    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(-1, (int)(unsigned)(v >> 32), CTRL, ROWMASK, 0xf, false);
+    return ((unsigned long long)hi << 32) | lo;
+}
+__device__ __forceinline__ unsigned long long wave_prefix_min_u64(unsigned long long v) {
+    v = min(v, dpp_min_src_u64<0x111>(v));        // row_shr:1
+    v = min(v, dpp_min_src_u64<0x112>(v));        // row_shr:2
+    v = min(v, dpp_min_src_u64<0x114>(v));        // row_shr:4
+    v = min(v, dpp_min_src_u64<0x118>(v));        // row_shr:8
+    v = min(v, dpp_min_src_u64<0x142, 0xa>(v));   // row_bcast:15
+    v = min(v, dpp_min_src_u64<0x143, 0xc>(v));   // row_bcast:31
+    return v;
+}
+__device__ __forceinline__ unsigned long long from_left_u64(unsigned long long v, unsigned long long fill) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp((int)(unsigned)fill, (int)(unsigned)v, 0x138, 0xf, 0xf, false);
+    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp((int)(unsigned)(fill >> 32), (int)(unsigned)(v >> 32), 0x138, 0xf, 0xf, false);
+    return ((unsigned long long)hi << 32) | lo;  // wave_shr:1
+}
+__device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v, int lane) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, lane);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), lane);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
 // Last end-of-generation update and bestp = gbest_pos (PSO.cpp:864-882).  Replays the
 // gbest / count sequence from gmin[], finds the last improving generation g* and takes
 // particles.col(first argmin pcost) of that generation; resets gmin[] for the next call.
@@ -677,7 +706,41 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
     double bp = 0.0;  // gbest_pos = zeros<vec> (PSO.cpp:739) if nothing beat 1e100
     double gcost = 1e100;
     int last = -1, count = 100;
-    for (int base = 0; base <= G; base += CH) {
+    if (G <= 63) {
+        // G + 1 <= 64 generations: the replay as scans over wave 0's lanes (lane k =
+        // generation k), not a serial loop.  Costs are >= 0 or NaN, so their u64 bits
+        // order like their values and NaN bits (never written, or all NaN) sort above
+        // every cost: a u64 minimum is fmin, and "fm < gcost" is a u64 compare.
+        if (t < 64) {
+            unsigned long long key = ~0ull;
+            if (t <= G) {
+                double m = __builtin_nan("");
+                for (int c = 0; c < GMIN_SHARDS; ++c) m = fmin(m, bits_to_f64(*gmin_cell(sw, t, c)));
+                key = f64_to_bits(m);
+            }
+            const int topo = (t >= 1 && t <= G) ? sw.sig[t].topo : -1;
+            const unsigned long long cap = f64_to_bits(1e100);  // gbest starts at 1e100
+            const unsigned long long incl = wave_prefix_min_u64(key);
+            const unsigned long long excl = min(from_left_u64(incl, ~0ull), cap);
+            const bool imp = t >= 1 && t <= G && key < excl;  // PSO.cpp:864-872
+            const unsigned long long mask = __ballot(imp);
+            const int last0 = (readlane_u64(key, 0) < cap) ? 0 : -1;  // generation 0 (:755-760)
+            last = mask ? 63 - __builtin_clzll(mask) : last0;
+            if (t >= 1 && t <= G && sw.trace_g) {
+                // count after generation t: 0 at an improvement, +1 otherwise, from 100
+                const unsigned long long upto = mask & ((2ull << t) - 1);
+                const int L = upto ? 63 - __builtin_clzll(upto) : 0;
+                sw.trace_g[t - 1] = bits_to_f64(min(incl, cap));
+                sw.trace_count[t - 1] = L >= 1 ? t - L : 100 + t;
+                sw.trace_topo[t - 1] = topo;
+            }
+            if (t == 0) {
+                sm.iscal[2] = last;
+                sm.dscal[5] = bits_to_f64(min(readlane_u64(incl, G), cap));
+            }
+        }
+    }
+    for (int base = 0; G > 63 && base <= G; base += CH) {
         // all loads of the pass at once, then a serial replay from LDS by thread 0
         for (int k = t; k < CH && base + k <= G; k += HPE_NT) {
             double m = __builtin_nan("");  // all-ones (never written) is a NaN too
@@ -715,30 +778,57 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
         }
         __syncthreads();
     }
-    if (t == 0) {
+    if (G > 63 && t == 0) {
         sm.iscal[2] = last;
         sm.dscal[5] = gcost;
     }
     __syncthreads();
     last = sm.iscal[2];
     gcost = sm.dscal[5];
-    if (last >= 0) {
-        const double *pc = sw.pch + (size_t)last * P;
-        VI mine = {__builtin_inf(), 0};
-        for (int k = t; k < P; k += HPE_NT) {
-            const double v = nan_inf(pc[k]);
-            if (v < mine.v) {
-                mine.v = v;
-                mine.i = k;
+    if (last >= 0 && P <= HPE_NT) {
+        // one particle per thread: its pbest cost and its position row of generation
+        // `last` in one round trip; the winner's thread writes bestp
+        const int k = t < P ? t : P - 1;
+        const double *row = sw.xh + ((size_t)last * P + k) * HPE_DOF;
+        double r[HPE_DOF];
+#pragma unroll
+        for (int d = 0; d < HPE_DOF; ++d) r[d] = row[d];
+        VI mine = {t < P ? nan_inf(sw.pch[(size_t)last * P + k]) : __builtin_inf(), t < P ? t : 0};
+        const VI b = block_argmin(sm, mine);
+        if (t == b.i) {
+#pragma unroll
+            for (int d = 0; d < HPE_DOF; ++d) {
+                out[d] = r[d];
+                sw.gpos[d] = r[d];
             }
         }
-        const VI b = block_argmin(sm, mine);
-        if (t < HPE_DOF) bp = sw.xh[((size_t)last * P + b.i) * HPE_DOF + t];
-    }
-    // bestp stays in each thread's register: no barrier and no re-read of `out`
-    if (t < HPE_DOF) {
-        out[t] = bp;
-        sw.gpos[t] = bp;
+        if (TAIL && !same_eval) {  // the tail below evaluates cal_cost(bestp)
+            if (t == b.i) {
+#pragma unroll
+                for (int d = 0; d < HPE_DOF; ++d) sm.pbr[d] = r[d];
+            }
+            __syncthreads();
+            if (t < HPE_DOF) bp = sm.pbr[t];
+        }
+    } else {
+        if (last >= 0) {
+            const double *pc = sw.pch + (size_t)last * P;
+            VI mine = {__builtin_inf(), 0};
+            for (int k = t; k < P; k += HPE_NT) {
+                const double v = nan_inf(pc[k]);
+                if (v < mine.v) {
+                    mine.v = v;
+                    mine.i = k;
+                }
+            }
+            const VI b = block_argmin(sm, mine);
+            if (t < HPE_DOF) bp = sw.xh[((size_t)last * P + b.i) * HPE_DOF + t];
+        }
+        // bestp stays in each thread's register: no barrier and no re-read of `out`
+        if (t < HPE_DOF) {
+            out[t] = bp;
+            sw.gpos[t] = bp;
+        }
     }
     if (t == 0) out[HPE_DOF] = gcost;
     for (int c = t; c < (G + 1) * GMIN_SHARDS; c += HPE_NT) sw.gmin[(size_t)c * GMIN_STRIDE] = ~0ull;

@@ -74,7 +74,7 @@ def total(policy, logs):
     return sum(rounds(policy, s) for s in logs)
 
 
-def prefix_closed(k, maxdepth=7):
+def prefix_closed(k, maxdepth=6):  # nodes up to 5 decisions deep: gold_shape's 5 bits
     res = set()
 
     def grow(S):
@@ -112,6 +112,7 @@ def packed(pol):
         idx = {s: i for i, s in enumerate(nodes)}
         nb = dn = up = 0
         for i, s in enumerate(nodes):
+            assert len(s) <= 5
             nb |= ((len(s) << 5) | sum(1 << k for k, ch in enumerate(s) if ch == "U")) << (8 * i)
         for i in range(8):
             s = nodes[i] if i < len(nodes) else None
