@@ -1104,12 +1104,13 @@ struct GoldShape {
 #define GOLD_8 1
 #define GOLD_7 2
 #define GOLD_4 3
+#define GOLD_OPT8 4  // pso_optimise's descent (tools/gold_shapes.py optimise)
 #ifndef HPE_GOLD_POLICY
 #define HPE_GOLD_POLICY GOLD_8  // refine_init_pose
 #endif
 template <int POL>
 __device__ __forceinline__ GoldShape gold_shape(int ctx) {
-    constexpr GoldShape T[12] = {
+    constexpr GoldShape T[15] = {
     // GOLD_BALANCED
     {7, 0x0043414240212000ull, 0xfffff531u, 0xfffff642u},  // first: '' 'D' 'U' 'DD' 'DU' 'UD' 'UU'
     {7, 0x0043414240212000ull, 0xfffff531u, 0xfffff642u},  // D: '' 'D' 'U' 'DD' 'DU' 'UD' 'UU'
@@ -1126,6 +1127,10 @@ __device__ __forceinline__ GoldShape gold_shape(int ctx) {
     {4, 0x0000000043212000ull, 0xfffffff1u, 0xfffff3f2u},  // first: '' 'D' 'U' 'UU'
     {4, 0x0000000060402000ull, 0xfffff321u, 0xffffffffu},  // D: '' 'D' 'DD' 'DDD'
     {4, 0x0000000040212000ull, 0xffffff31u, 0xfffffff2u},  // U: '' 'D' 'U' 'DD'
+    // GOLD_OPT8
+    {8, 0xbf8f674340212000ull, 0xffffff31u, 0xf765f4f2u},  // first: '' 'D' 'U' 'DD' 'UU' 'UUU' 'UUUU' 'UUUUU'
+    {8, 0x6043414240212000ull, 0xffff7531u, 0xfffff642u},  // D: '' 'D' 'U' 'DD' 'DU' 'UD' 'UU' 'DDD'
+    {8, 0x6743414240212000ull, 0xfffff531u, 0xf7fff642u},  // U: '' 'D' 'U' 'DD' 'DU' 'UD' 'UU' 'UUU'
     };
     return ctx == 0 ? T[3 * POL] : ctx == 1 ? T[3 * POL + 1] : T[3 * POL + 2];
 }

@@ -158,7 +158,7 @@ __global__ __launch_bounds__(RF_NT) void k_opt_descent(DevOpt op, const DevObs *
         __syncthreads();  // p published; rs.f is the Goldstein nodes' next
         sc.lap(27);
         double facc = fk;
-        const double tk = gold_tree(rs, o, cv, H, match, fk, gp, evals, &facc);
+        const double tk = gold_tree<false, GOLD_OPT8>(rs, o, cv, H, match, fk, gp, evals, &facc);
         sc.start();
         if (t < HPE_DOF) rs.x0[t] = rs.x0[t] - tk * gl;
         __syncthreads();
