@@ -390,6 +390,7 @@ def main():
         dump_state()
     ctx.check(lib.hpe_sync(ctx.h))
     torch.cuda.synchronize()
+    state0 = state.clone()  # the diagnostic passes below restart from here: same frames, same work
     # timed region: graph-replayed frames, nothing else on the tracker stream
     if world > 1:
         dist.barrier()
@@ -418,6 +419,8 @@ def main():
     # tracker stream (not in the timed region: each timing event adds a marker, ~5 us)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
+    state.copy_(state0)
+    torch.cuda.synchronize()
     if not args.resident:
         ctx.pipeline_begin(raw[args.warmup], True, ds)
     for k, f in enumerate(range(args.warmup, n_frames)):
@@ -433,6 +436,8 @@ def main():
     ctx.check(lib.hpe_profile_enable(ctx.h, 1))
     rev = C.c_uint64(0)
     ctx.check(lib.hpe_refine_eval_count(ctx.h, C.byref(rev), 1))  # reset
+    state.copy_(state0)
+    torch.cuda.synchronize()
     if not args.resident:
         ctx.pipeline_begin(raw[args.warmup], True, ds)
     errs = []  # gnd_truth_err (costfunc.cpp:476-507) of each frame's bestp vs the true pose
@@ -463,6 +468,8 @@ def main():
     ctx.check(lib.hpe_profile_enable(ctx.h, 0))
     prof["frame_graph"] = {"launches": len(frame_us), "avg_us": sum(frame_us) / len(frame_us),
                            "min_us": min(frame_us), "max_us": max(frame_us),
+                           "median_us": float(np.median(frame_us)),
+                           "per_frame_us": [round(x, 1) for x in frame_us],
                            "note": "one event pair per frame, a second pass over the frames"}
     lib_path = hpe._lib.load()._name
 
