@@ -867,8 +867,9 @@ struct __align__(16) RefineSm {
     FkSm w[RF_NW];
     FkSm base;  // spheres of the current x0
     double red[16][4];
-    double x0[32], g[32], p[32];
+    double x0[32];
     double f[RF_NW];
+    double fg[RF_NW];  // the gradient points' costs (k_refine, single-workgroup form)
     FkX X;  // rotation-only joint terms of x0 (refine block 2: translation steps)
     unsigned ts_n;  // diagnostic build: refine timeline entries written
 };
@@ -1135,18 +1136,20 @@ __device__ __forceinline__ GoldShape gold_shape(int ctx) {
     return ctx == 0 ? T[3 * POL] : ctx == 1 ? T[3 * POL + 1] : T[3 * POL + 2];
 }
 
-// goldstein(x, g, matchId, f_k, optfunc, tk, 30) (PSO.cpp:438-480) along rs.p from rs.x0
+// goldstein(x, g, matchId, f_k, optfunc, tk, 30) (PSO.cpp:438-480) along p from rs.x0
 // with frozen correspondences, speculated per round with shape policy POL (above): wave w
 // evaluates node w, then every thread walks the nodes with the serial algorithm's rules.
-// Returns tk (0 after 30 rejected trials); the accepted node's spheres are copied into
-// rs.base and its cost to *f_acc.  evals grows by the serial evaluation count.
-template <bool MW = false, int POL = GOLD_BALANCED, class CV>
+// pl: component (threadIdx.x & 63) of the direction p, in every thread.  Returns tk (0
+// after 30 rejected trials); the accepted node's spheres are copied into rs.base and its
+// cost to *f_acc.  UPD: the search also applies x0 = x0 - tk * g (PSO.cpp:256; gl =
+// component threadIdx.x of g) before its last barrier.  evals grows by the serial count.
+template <bool MW = false, int POL = GOLD_BALANCED, bool UPD = false, class CV>
 __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const CV &cv,
                                             const DevHand *__restrict__ H,
                                             const int32_t *__restrict__ match, double fk,
-                                            double gp, int &evals, double *f_acc,
-                                            FkX *Xt = nullptr, MwLeader *ml = nullptr,
-                                            int *flag = nullptr) {
+                                            double gp, double pl, double gl, int &evals,
+                                            double *f_acc, FkX *Xt = nullptr,
+                                            MwLeader *ml = nullptr, int *flag = nullptr) {
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
     StampClock sc;
     sc.start();
@@ -1164,7 +1167,7 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
                 if ((bits >> k) & 1) gold_up(a, b, al2);
                 else gold_down(a, b, al2);
             }
-            if (l < HPE_DOF) rs.w[w].th[l] = rs.x0[l] + al2 * rs.p[l];
+            if (l < HPE_DOF) rs.w[w].th[l] = rs.x0[l] + al2 * pl;
         }
         eval_nodes<MW>(rs, nn, o, cv, H, match, Xt, ml, flag);
         if (MW && ml->failed) break;  // the launch is ending early (DevMw::err)
@@ -1202,6 +1205,8 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
             }
         }
         if (!done && it >= 30) done = true;  // tk stays 0
+        // x0 is read only before eval_nodes' barrier in a round
+        if (UPD && done && t < HPE_DOF) rs.x0[t] = rs.x0[t] - tk * gl;
         if (done && accepted >= 0) {  // keep the accepted node's spheres for the next f_k
             for (int q = t; q < (int)(offsetof(FkSm, J) / 8); q += RF_NT)
                 ((double *)&rs.base)[q] = ((const double *)&rs.w[accepted])[q];
@@ -1368,21 +1373,24 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
                 REF_TS(rs.ts_n, 2);
                 if (w < 6) {
                     const double f = frozen_tail(rs.w[w], o, cv, H, match, hd);
-                    if (l == 0) rs.f[w] = f;
+                    if (l == 0) rs.fg[w] = f;
                 }
                 __syncthreads();
             }
             ++evals;
             sc.lap(20);
             evals += 6;
-            if (t < HPE_DOF) {  // PSO.cpp:197-212; p = -1 * grad
-                const double g = (t >= lo && t <= lo + 2)
-                                     ? (rs.f[2 * (t - lo)] - rs.f[2 * (t - lo) + 1]) / (2 * e)
-                                     : 0.0;
-                rs.g[t] = g;
-                rs.p[t] = -1 * g;
-            }
-            __syncthreads();
+            // cal_grad (PSO.cpp:197-212): g on the block dims, p = -1 * g, computed by every
+            // thread for its lane -- no barrier: fg is rewritten only by the next iteration's
+            // gradient points (the multi-workgroup form's rs.f by this search's first round,
+            // hence its barrier)
+            const double *fg = MW ? rs.f : rs.fg;
+            const double g0 = (fg[0] - fg[1]) / (2 * e), g1 = (fg[2] - fg[3]) / (2 * e),
+                         g2 = (fg[4] - fg[5]) / (2 * e);
+            const int dl = l - lo;
+            const double gl = (dl == 0) ? g0 : (dl == 1) ? g1 : (dl == 2) ? g2 : 0.0;
+            const double pl = -1 * gl;
+            if (MW) __syncthreads();
             REF_TS(rs.ts_n, 3);
             sc.lap(21);
             // g'p by op_dot::direct_dot_arma (two accumulators: even / odd indices).  g is
@@ -1390,21 +1398,20 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
             // (x + -0 = x; the empty sums stay zero), so the sums reduce to the block's
             // terms in the same order: block 0 (dims 0..2) v1 = g0 p0 + g2 p2, v2 = g1 p1;
             // block 1 (dims 3..5) v1 = g4 p4, v2 = g3 p3 + g5 p5.  Same for |g|^2 (tol).
-            const double g0 = rs.g[lo], g1 = rs.g[lo + 1], g2 = rs.g[lo + 2];
             const double q0 = g0 * (-1 * g0), q1 = g1 * (-1 * g1), q2 = g2 * (-1 * g2);
             const double s0 = g0 * g0, s1 = g1 * g1, s2 = g2 * g2;
             const double gp = (blk == 0) ? (q0 + q2) + q1 : q1 + (q0 + q2);
             // goldstein(x0, grad, matchId, f_k, optfunc, tk, 30)
-            const double tk = gold_tree<MW, HPE_GOLD_POLICY>(rs, o, cv, H, match, fk, gp, evals, nullptr, Xt, &ml, &mwflag);
+            // goldstein(x0, grad, matchId, f_k, optfunc, tk, 30), then x0 = x0 - tk*grad
+            const double tk = gold_tree<MW, HPE_GOLD_POLICY, true>(rs, o, cv, H, match, fk, gp, pl, gl,
+                                                                  evals, nullptr, Xt, &ml, &mwflag);
             sc.lap(22);
             if (tk == 0) cnt += 1;
             // tol = sqrt(sum(grad % grad)): arrayops::accumulate (two accumulators)
             tol = sqrt((blk == 0) ? (s0 + s2) + s1 : s1 + (s0 + s2));
             iter += 1;
-            // (gold_tree ended with a barrier: every read of x0 in it is done)
-            if (t < HPE_DOF) rs.x0[t] = rs.x0[t] - tk * rs.g[t];
+            // gold_tree's last barrier published x0 and the accepted node's spheres
             base_valid = true;  // accepted node copied, or tk == 0 and x0 unchanged
-            __syncthreads();
             REF_TS(rs.ts_n, 5);
             sc.lap(23);
         }

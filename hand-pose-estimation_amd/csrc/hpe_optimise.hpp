@@ -153,12 +153,12 @@ __global__ __launch_bounds__(RF_NT) void k_opt_descent(DevOpt op, const DevObs *
         // g is gs on coordinate sel, 0 elsewhere, p = -1 * g; dot(g, p) by two accumulators
         // (op_dot::direct_dot_arma) has the one nonzero term, exactly
         const double gl = (t == sel) ? gs : 0.0;
+        const double pl = -1 * ((l == sel) ? gs : 0.0);  // p = -1 * g, this thread's lane
         const double gp = gs * (-1 * gs);
-        if (t < HPE_DOF) rs.p[t] = -1 * gl;
-        __syncthreads();  // p published; rs.f is the Goldstein nodes' next
+        __syncthreads();  // rs.f is the Goldstein nodes' next
         sc.lap(27);
         double facc = fk;
-        const double tk = gold_tree<false, GOLD_OPT8>(rs, o, cv, H, match, fk, gp, evals, &facc);
+        const double tk = gold_tree<false, GOLD_OPT8>(rs, o, cv, H, match, fk, gp, pl, 0.0, evals, &facc);
         sc.start();
         if (t < HPE_DOF) rs.x0[t] = rs.x0[t] - tk * gl;
         __syncthreads();
