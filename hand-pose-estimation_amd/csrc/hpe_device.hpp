@@ -511,6 +511,23 @@ __device__ __forceinline__ void block_sum3(double (*red)[4], double &a, double &
     if (REUSE) __syncthreads();
 }
 
+// Sum one per-thread double over NT threads in a fixed order; result in every thread.
+// The cost kernels sum each lane's total (align * lambda + depth + collision) once
+// instead of the three terms separately: the same cost to the last bits (the reference's
+// own sums run in yet another order) for one wave reduction instead of three.
+template <int NT, bool REUSE = true>
+__device__ __forceinline__ double block_sum1(double (*red)[4], double v) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) red[w][0] = v;
+    __syncthreads();
+    double r = 0;
+#pragma unroll
+    for (int k = 0; k < NT / 64; ++k) r += red[k][0];
+    if (REUSE) __syncthreads();
+    return r;
+}
+
 // ---------------------------------------------------------------- cost terms
 // depth_penalty term of sphere i (costfunc.cpp:249-300); S is un-negated on the fly.
 // Two halves, so that the gathers' L2 round trip overlaps the caller's other work:
@@ -859,9 +876,7 @@ __device__ __forceinline__ double eval_wave_cost(FkSm &f, const DevObs &o, const
     const DepthG dg = depth_issue_at(own, l, o, H);
     double al = search_align<64, false>(f, cv, H, nullptr, pre, l);
     double dep = depth_finish(dg, o, l < HPE_NS);
-    double co = 0.0;
-    wave_sum3(al, dep, co);
-    return al * o.lambda + dep;
+    return wave_sum(al * o.lambda + dep);
 }
 
 __device__ __forceinline__ CloudGlobal obs_cloud(const DevObs &o) {
@@ -913,7 +928,19 @@ __device__ __forceinline__ double eval_block(Smem &sm, const DevObs &o, const CV
     if (HPE_STAMPS) asm volatile("" ::"v"(al), "v"(dep));
     WAVE_TS(g_ts, 16);
     sc.lap(11);
-    block_sum3<NT, false, !(MODE == EV_COST2_CORR || MODE == EV_COST2_FROZEN)>(sm.red, al, dep, co);
+    if constexpr (!(MODE == EV_COST2_CORR || MODE == EV_COST2_FROZEN)) {
+        // cal_cost (the PSO's evaluations): the lane totals summed once (block_sum1); the
+        // separate terms are not formed
+        const double tot = block_sum1<NT, false>(sm.red, al * o.lambda + dep);
+        sc.lap(12);
+        if (t == 0) {
+            sm.dscal[0] = __builtin_nan("");
+            sm.dscal[1] = __builtin_nan("");
+            sm.dscal[2] = 0.0;
+        }
+        return tot;
+    }
+    block_sum3<NT, false>(sm.red, al, dep, co);
     sc.lap(12);
     const double align = al * o.lambda;
     if (t == 0) {
@@ -978,9 +1005,10 @@ __device__ __forceinline__ double frozen_tail(const FkSm &f, const DevObs &o, co
     double al = align_frozen(f, cv, H, match, l, 64);
     double co = hd.co;
     asm volatile("" ::"v"(co));  // complete before depth_finish's wait for the gathers
-    double dep = depth_finish(hd.dg, o, l < HPE_NS);
-    wave_sum3(al, dep, co);
-    return (al * o.lambda + dep) + co;
+    const double dep = depth_finish(hd.dg, o, l < HPE_NS);
+    // one wave sum of the lane totals (the three terms' sums in another order: the same
+    // value to the last bits, as any order of the reference's own sums)
+    return wave_sum((al * o.lambda + dep) + co);
 }
 template <bool OUTLINE_TRIG = false, class CV>
 __device__ __forceinline__ double eval_wave_frozen(FkSm &f, const DevObs &o,

@@ -1346,13 +1346,9 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
                 double al = search_align<RF_NT, true>(rs.base, cv, H, match, load_pt(cv, t));
                 if (young) __builtin_amdgcn_s_setprio(0);
                 double co = (t < 144) ? collide_term(rs.base, t, H) : 0.0;
-                double dep = depth_finish(dgc, o, t < HPE_NS);
-                wave_sum3(al, dep, co);  // the corr sums, as block_sum3 orders them
-                if (l == 0) {
-                    rs.red[w][0] = al;
-                    rs.red[w][1] = dep;
-                    rs.red[w][2] = co;
-                }
+                const double dep = depth_finish(dgc, o, t < HPE_NS);
+                const double tot = wave_sum((al * o.lambda + dep) + co);  // as block_sum1
+                if (l == 0) rs.red[w][0] = tot;
                 FrozenHead hd{};
                 if (w < 6) {
                     const int d = lo + (w >> 1);
@@ -1362,14 +1358,9 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
                     hd = frozen_head<true>(rs.w[w], o, H, Xt);
                 }
                 __syncthreads();  // matchId complete, the corr partial sums in red
-                double ra = 0, rb = 0, rc = 0;
+                fk = 0;
 #pragma unroll
-                for (int k = 0; k < RF_NW; ++k) {
-                    ra += rs.red[k][0];
-                    rb += rs.red[k][1];
-                    rc += rs.red[k][2];
-                }
-                fk = (ra * o.lambda + rb) + rc;
+                for (int k = 0; k < RF_NW; ++k) fk += rs.red[k][0];
                 REF_TS(rs.ts_n, 2);
                 if (w < 6) {
                     const double f = frozen_tail(rs.w[w], o, cv, H, match, hd);

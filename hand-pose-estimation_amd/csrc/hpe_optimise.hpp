@@ -137,8 +137,7 @@ __global__ __launch_bounds__(RF_NT) void k_opt_descent(DevOpt op, const DevObs *
             double al = search_align<RF_NT, true>(rs.base, cv, H, match, load_pt(cv, t));
             double co = (t < 144) ? collide_term(rs.base, t, H) : 0.0;
             double dep = depth_finish(dg, o, t < HPE_NS);
-            block_sum3<RF_NT>(rs.red, al, dep, co);
-            fk = (al * o.lambda + dep) + co;
+            fk = block_sum1<RF_NT>(rs.red, (al * o.lambda + dep) + co);
             sc.lap(26);
         }
         const int sel = sel_s[m];
@@ -169,8 +168,7 @@ __global__ __launch_bounds__(RF_NT) void k_opt_descent(DevOpt op, const DevObs *
                 double al = search_align<RF_NT, true>(rs.base, cv, H, match, load_pt(cv, t));
                 double co = (t < 144) ? collide_term(rs.base, t, H) : 0.0;
                 double dep = depth_finish(dg, o, t < HPE_NS);
-                block_sum3<RF_NT>(rs.red, al, dep, co);
-                f2 = (al * o.lambda + dep) + co;
+                f2 = block_sum1<RF_NT>(rs.red, (al * o.lambda + dep) + co);
             } else {
                 f2 = facc;
             }
