@@ -245,9 +245,12 @@ struct SphXYZ {
     double x, y, z;
 };
 
+// thr (optional): theta[l] of this lane l < 26, already in a register where the caller
+// computed it (it still stores f.th for the chain phase): the trig phase then runs on
+// lanes 0..2 and 6..25 from that register, without the LDS round trip of the permuted read.
 template <int MODE, bool OUTLINE_TRIG = false>
 __device__ __forceinline__ void fk_wave_t(FkSm &f, const DevHand *__restrict__ H, FkX *X,
-                                          SphXYZ *own = nullptr) {
+                                          SphXYZ *own = nullptr, const double *thr = nullptr) {
     const int l = threadIdx.x & 63;
     StampClock sc;
     sc.start();
@@ -262,12 +265,14 @@ __device__ __forceinline__ void fk_wave_t(FkSm &f, const DevHand *__restrict__ H
     const int sd = H->dg[sl], sa = H->ja[sl];
     const double swa = H->wa[sl], swb = H->wb[sl];
     if (MODE != FK_TRANSLATE) {
-        if (l < 23) {
+        // slot k of sn / cs: TWS (fingermodel.cpp:91), ANG, ROT, then the 20 digit angles
+        // (handmodel.cpp:141-146) = theta[k < 3 ? k : k + 3]
+        const int k = thr ? (l < 3 ? l : l - 3) : l;
+        if (thr ? (l < 3 || (l >= 6 && l < 26)) : (l < 23)) {
             // one unconditional LDS read per lane (per-lane branches would serialise three
-            // read round trips): TWS (fingermodel.cpp:91), ANG, ROT, digit angles
-            // (handmodel.cpp:141-146)
-            const double th = f.th[l < 3 ? l : 6 + (l - 3)];
-            const double a = deg2rad(l == 0 ? th + 180 : th);
+            // read round trips)
+            const double th = thr ? *thr : f.th[l < 3 ? l : 6 + (l - 3)];
+            const double a = deg2rad(k == 0 ? th + 180 : th);
             double s, c;
             if (OUTLINE_TRIG) {
                 const SinCos r = sincos_outline(a);
@@ -276,8 +281,8 @@ __device__ __forceinline__ void fk_wave_t(FkSm &f, const DevHand *__restrict__ H
             } else {
                 sincos(a, &s, &c);
             }
-            f.sn[l] = s;
-            f.cs[l] = c;
+            f.sn[k] = s;
+            f.cs[k] = c;
         }
         wave_sync();
     }
@@ -385,8 +390,8 @@ __device__ __forceinline__ void fk_wave_t(FkSm &f, const DevHand *__restrict__ H
 
 template <bool OUTLINE_TRIG = false>
 __device__ __forceinline__ void fk_wave(FkSm &f, const DevHand *__restrict__ H,
-                                        SphXYZ *own = nullptr) {
-    fk_wave_t<FK_FULL, OUTLINE_TRIG>(f, H, nullptr, own);
+                                        SphXYZ *own = nullptr, const double *thr = nullptr) {
+    fk_wave_t<FK_FULL, OUTLINE_TRIG>(f, H, nullptr, own, thr);
 }
 
 // ---------------------------------------------------------------- reductions
@@ -968,10 +973,10 @@ struct FrozenHead {
 template <bool OUTLINE_TRIG = false>
 __device__ __forceinline__ FrozenHead frozen_head(FkSm &f, const DevObs &o,
                                                   const DevHand *__restrict__ H,
-                                                  FkX *Xt = nullptr) {
+                                                  FkX *Xt = nullptr, const double *thr = nullptr) {
     SphXYZ own;
     if (Xt) fk_wave_t<FK_TRANSLATE>(f, H, Xt, &own);
-    else fk_wave<OUTLINE_TRIG>(f, H, &own);
+    else fk_wave<OUTLINE_TRIG>(f, H, &own, thr);
     const int l = threadIdx.x & 63;
     FrozenHead r;
     r.dg = depth_issue_at(own, l, o, H);
@@ -1015,8 +1020,8 @@ __device__ __forceinline__ double eval_wave_frozen(FkSm &f, const DevObs &o,
                                                    const CV &cv,
                                                    const DevHand *__restrict__ H,
                                                    const int32_t *__restrict__ match,
-                                                   FkX *Xt = nullptr) {
-    return frozen_tail(f, o, cv, H, match, frozen_head<OUTLINE_TRIG>(f, o, H, Xt));
+                                                   FkX *Xt = nullptr, const double *thr = nullptr) {
+    return frozen_tail(f, o, cv, H, match, frozen_head<OUTLINE_TRIG>(f, o, H, Xt, thr));
 }
 
 // ---------------------------------------------------------------- Philox4x32-10

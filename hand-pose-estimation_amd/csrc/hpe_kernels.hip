@@ -380,6 +380,7 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
     SphXYZ own0{0.0, 0.0, 0.0};  // wave 0: the centres FK leaves in registers
     BLK_TS(g, 2);
     if (t < 64) {
+        double thl = 0.0;  // x of this lane's dimension, handed to FK's trig in a register
         // ---- velocity, position, check_constraints (PSO.cpp:824-842, 358-377)
         if (t < HPE_DOF) {
             rp = sm.draws[t];
@@ -398,11 +399,12 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
             sw.v[e] = vn;
             sw.xh[(size_t)g * P * HPE_DOF + e] = xn;
             sm.fk.th[t] = xn;
+            thl = xn;
         }
         wave_sync();
         BLK_TS(g, 10);
         sc.lap(2);
-        fk_wave(sm.fk, H, &own0);
+        fk_wave(sm.fk, H, &own0, &thl);
     }
     __syncthreads();  // spheres, topology and own pbest cost published
     BLK_TS(g, 3);
@@ -964,12 +966,12 @@ template <bool MW, class CV>
 __device__ __forceinline__ void eval_nodes(RefineSm &rs, int nn, const DevObs &o, const CV &cv,
                                            const DevHand *__restrict__ H,
                                            const int32_t *__restrict__ match, FkX *Xt,
-                                           MwLeader *ml, int *flag) {
+                                           MwLeader *ml, int *flag, const double *thr = nullptr) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     if (!MW) {
         if (w < nn) {
             wave_sync();
-            const double f = eval_wave_frozen<true>(rs.w[w], o, cv, H, match, Xt);
+            const double f = eval_wave_frozen<true>(rs.w[w], o, cv, H, match, Xt, thr);
             if (l == 0) rs.f[w] = f;
         }
         REF_TS(rs.ts_n, 9);  // wave 0's node done
@@ -1160,6 +1162,7 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
     while (!done) {
         const GoldShape sh = gold_shape<POL>(ctx);
         const int nn = sh.n;
+        double thl = 0.0;  // theta[l] of this wave's node (FK's trig reads it in a register)
         if (w < nn) {
             double a = A, b = B, al2 = alpha;
             const int nbw = (int)((sh.nb >> (8 * w)) & 0xff), len = nbw >> 5, bits = nbw & 31;
@@ -1167,9 +1170,10 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
                 if ((bits >> k) & 1) gold_up(a, b, al2);
                 else gold_down(a, b, al2);
             }
-            if (l < HPE_DOF) rs.w[w].th[l] = rs.x0[l] + al2 * pl;
+            thl = rs.x0[l < HPE_DOF ? l : 0] + al2 * pl;
+            if (l < HPE_DOF) rs.w[w].th[l] = thl;
         }
-        eval_nodes<MW>(rs, nn, o, cv, H, match, Xt, ml, flag);
+        eval_nodes<MW>(rs, nn, o, cv, H, match, Xt, ml, flag, &thl);
         if (MW && ml->failed) break;  // the launch is ending early (DevMw::err)
         int node = 0;
         accepted = -1;
@@ -1352,10 +1356,11 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
                 FrozenHead hd{};
                 if (w < 6) {
                     const int d = lo + (w >> 1);
-                    if (l < HPE_DOF)
-                        rs.w[w].th[l] = (l == d) ? ((w & 1) ? rs.x0[l] - e : rs.x0[l] + e) : rs.x0[l];
+                    const double xl = rs.x0[l < HPE_DOF ? l : 0];
+                    const double thl = (l == d) ? ((w & 1) ? xl - e : xl + e) : xl;
+                    if (l < HPE_DOF) rs.w[w].th[l] = thl;
                     wave_sync();
-                    hd = frozen_head<true>(rs.w[w], o, H, Xt);
+                    hd = frozen_head<true>(rs.w[w], o, H, Xt, &thl);
                 }
                 __syncthreads();  // matchId complete, the corr partial sums in red
                 fk = 0;
