@@ -864,6 +864,63 @@ __device__ __forceinline__ double align_frozen(const FkSm &f, const CV &cv,
     return (a0 + a1) + (a2 + a3);
 }
 
+// The frozen matchIds of one lane for clouds of at most 256 points (the reference's
+// down-sampled cloud, N = 250): those of points l + 64 k, loaded once per refine iteration
+// after the correspondence search, so a node evaluation's alignment issues the point and
+// matched-sphere reads together (one LDS round trip instead of two).
+#define FP_MAX 256
+struct FrozenPts {
+    int id[4];
+};
+template <class CV>
+__device__ __forceinline__ void load_frozen_pts(FrozenPts &fp, const CV &cv,
+                                                const int32_t *__restrict__ match, int l) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) fp.id[k] = match[min(l + 64 * k, cv.n - 1)];
+}
+// align_frozen over the lane's points (n <= FP_MAX): the same per-point operations
+template <class CV>
+__device__ __forceinline__ double align_frozen_pts(const FkSm &f, const FrozenPts &fp,
+                                                   const CV &cv, const DevHand *__restrict__ H,
+                                                   int l) {
+    double px[4], py[4], pz[4], sx[4], sy[4], sz[4], sr[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int q = min(l + 64 * k, cv.n - 1);
+        px[k] = cv.cx[q];
+        py[k] = cv.cy[q];
+        pz[k] = cv.cz[q];
+        sx[k] = f.S[fp.id[k]][0];
+        sy[k] = f.S[fp.id[k]][1];
+        sz[k] = f.S[fp.id[k]][2];
+        sr[k] = H->radii[fp.id[k]];
+    }
+    asm volatile("" : "+v"(sx[0]), "+v"(sx[1]), "+v"(sx[2]), "+v"(sx[3]), "+v"(sy[0]),
+                 "+v"(sy[1]), "+v"(sy[2]), "+v"(sy[3]), "+v"(sz[0]), "+v"(sz[1]),
+                 "+v"(sz[2]), "+v"(sz[3]), "+v"(sr[0]), "+v"(sr[1]), "+v"(sr[2]), "+v"(sr[3]),
+                 "+v"(px[0]), "+v"(px[1]), "+v"(px[2]), "+v"(px[3]), "+v"(py[0]), "+v"(py[1]),
+                 "+v"(py[2]), "+v"(py[3]), "+v"(pz[0]), "+v"(pz[1]), "+v"(pz[2]), "+v"(pz[3]));
+    const int n = cv.n;
+    double d2[4], rt[4], e[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const double dx = px[k] - sx[k], dy = py[k] - sy[k], dz = pz[k] - sz[k];
+        d2[k] = (dx * dx + dy * dy) + dz * dz;
+        rt[k] = hpe_sqrt_nr(d2[k]);
+    }
+    if (!(hpe_sqrt_direct(d2[0]) && hpe_sqrt_direct(d2[1]) && hpe_sqrt_direct(d2[2]) &&
+          hpe_sqrt_direct(d2[3]))) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) rt[k] = hpe_sqrt_direct(d2[k]) ? rt[k] : sqrt(d2[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const double r = rt[k] - sr[k];
+        e[k] = (l + 64 * k < n) ? r * r : 0.0;
+    }
+    return (e[0] + e[1]) + (e[2] + e[3]);
+}
+
 #ifndef HPE_SETPRIO_FROM
 #define HPE_SETPRIO_FROM 4  // first wave of a 512-thread block raised during the search
 #endif
@@ -1005,9 +1062,9 @@ template <class CV>
 __device__ __forceinline__ double frozen_tail(const FkSm &f, const DevObs &o, const CV &cv,
                                               const DevHand *__restrict__ H,
                                               const int32_t *__restrict__ match,
-                                              FrozenHead hd) {
+                                              FrozenHead hd, const FrozenPts *fp = nullptr) {
     const int l = threadIdx.x & 63;
-    double al = align_frozen(f, cv, H, match, l, 64);
+    double al = fp ? align_frozen_pts(f, *fp, cv, H, l) : align_frozen(f, cv, H, match, l, 64);
     double co = hd.co;
     asm volatile("" ::"v"(co));  // complete before depth_finish's wait for the gathers
     const double dep = depth_finish(hd.dg, o, l < HPE_NS);
@@ -1020,8 +1077,9 @@ __device__ __forceinline__ double eval_wave_frozen(FkSm &f, const DevObs &o,
                                                    const CV &cv,
                                                    const DevHand *__restrict__ H,
                                                    const int32_t *__restrict__ match,
-                                                   FkX *Xt = nullptr, const double *thr = nullptr) {
-    return frozen_tail(f, o, cv, H, match, frozen_head<OUTLINE_TRIG>(f, o, H, Xt, thr));
+                                                   FkX *Xt = nullptr, const double *thr = nullptr,
+                                                   const FrozenPts *fp = nullptr) {
+    return frozen_tail(f, o, cv, H, match, frozen_head<OUTLINE_TRIG>(f, o, H, Xt, thr), fp);
 }
 
 // ---------------------------------------------------------------- Philox4x32-10

@@ -966,12 +966,13 @@ template <bool MW, class CV>
 __device__ __forceinline__ void eval_nodes(RefineSm &rs, int nn, const DevObs &o, const CV &cv,
                                            const DevHand *__restrict__ H,
                                            const int32_t *__restrict__ match, FkX *Xt,
-                                           MwLeader *ml, int *flag, const double *thr = nullptr) {
+                                           MwLeader *ml, int *flag, const double *thr = nullptr,
+                                           const FrozenPts *fp = nullptr) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     if (!MW) {
         if (w < nn) {
             wave_sync();
-            const double f = eval_wave_frozen<true>(rs.w[w], o, cv, H, match, Xt, thr);
+            const double f = eval_wave_frozen<true>(rs.w[w], o, cv, H, match, Xt, thr, fp);
             if (l == 0) rs.f[w] = f;
         }
         REF_TS(rs.ts_n, 9);  // wave 0's node done
@@ -1151,7 +1152,8 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
                                             const int32_t *__restrict__ match, double fk,
                                             double gp, double pl, double gl, int &evals,
                                             double *f_acc, FkX *Xt = nullptr,
-                                            MwLeader *ml = nullptr, int *flag = nullptr) {
+                                            MwLeader *ml = nullptr, int *flag = nullptr,
+                                            const FrozenPts *fp = nullptr) {
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
     StampClock sc;
     sc.start();
@@ -1173,7 +1175,7 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
             thl = rs.x0[l < HPE_DOF ? l : 0] + al2 * pl;
             if (l < HPE_DOF) rs.w[w].th[l] = thl;
         }
-        eval_nodes<MW>(rs, nn, o, cv, H, match, Xt, ml, flag, &thl);
+        eval_nodes<MW>(rs, nn, o, cv, H, match, Xt, ml, flag, &thl, fp);
         if (MW && ml->failed) break;  // the launch is ending early (DevMw::err)
         int node = 0;
         accepted = -1;
@@ -1297,6 +1299,9 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
     int evals = 0;
     bool base_valid = false;
     const double e = 1e-5;  // cal_grad step (PSO.cpp:195)
+    // clouds of at most FP_MAX points: each lane keeps its frozen points in registers
+    const bool small = !MW && STAGED && o.n <= FP_MAX;
+    FrozenPts fpts;
     for (int blk = 0; blk < 2; ++blk) {
         const int lo = 3 * blk;  // start_idx (PSO.cpp:226-227); end_idx = lo + 2
         // Block 2 moves only the global position u = x0[3..5]: every FK of the block is
@@ -1363,12 +1368,13 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
                     hd = frozen_head<true>(rs.w[w], o, H, Xt, &thl);
                 }
                 __syncthreads();  // matchId complete, the corr partial sums in red
+                if (small) load_frozen_pts(fpts, cv, match, l);
                 fk = 0;
 #pragma unroll
                 for (int k = 0; k < RF_NW; ++k) fk += rs.red[k][0];
                 REF_TS(rs.ts_n, 2);
                 if (w < 6) {
-                    const double f = frozen_tail(rs.w[w], o, cv, H, match, hd);
+                    const double f = frozen_tail(rs.w[w], o, cv, H, match, hd, small ? &fpts : nullptr);
                     if (l == 0) rs.fg[w] = f;
                 }
                 __syncthreads();
@@ -1400,7 +1406,8 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
             // goldstein(x0, grad, matchId, f_k, optfunc, tk, 30)
             // goldstein(x0, grad, matchId, f_k, optfunc, tk, 30), then x0 = x0 - tk*grad
             const double tk = gold_tree<MW, HPE_GOLD_POLICY, true>(rs, o, cv, H, match, fk, gp, pl, gl,
-                                                                  evals, nullptr, Xt, &ml, &mwflag);
+                                                                  evals, nullptr, Xt, &ml, &mwflag,
+                                                                  small ? &fpts : nullptr);
             sc.lap(22);
             if (tk == 0) cnt += 1;
             // tol = sqrt(sum(grad % grad)): arrayops::accumulate (two accumulators)
