@@ -261,7 +261,8 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
     // (a non-volatile asm: it touches no memory, so later loads keep their scalar form)
     int z0 = 0;
     asm("" : "+s"(z0) : "s"(g), "s"(sw.gmin), "s"(sw.sig), "s"(sw.outl), "s"(sw.bounds),
-        "s"(sw.xh), "s"(sw.pch), "s"(sw.pb), "s"(sw.v), "s"(sw.inbox), "s"(sw.P), "s"(sw.K));
+        "s"(sw.xh), "s"(sw.pch), "s"(sw.pb), "s"(sw.v), "s"(sw.inbox), "s"(sw.P), "s"(sw.K),
+        "s"(og), "s"(Hg));
     StampClock sc;
     sc.begin();
     const DevObs o = *og;  // the selected frame (device-resident: graph-stable args)
@@ -269,11 +270,17 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
     __shared__ double ib[2][IB_KMAX][IB_FIELDS];
     const int i = blockIdx.x + z0, t = threadIdx.x, P = sw.P, K = sw.K;
     // valid slots of this receiver's kept (0) / rebuilt (1) inbox: only these are read
-    const int k0 = (P <= KIN_MAX) ? kin.k0[i] : K, k1 = (P <= KIN_MAX) ? kin.k1[i] : K;
+    // (read at blockIdx.x, clamped, unconditionally: the address depends on no loaded
+    // argument, so these loads leave with the argument loads instead of after them)
+    const int kb = (int)blockIdx.x & (KIN_MAX - 1);
+    const int k0r = kin.k0[kb], k1r = kin.k1[kb];
+    const int k0 = (P <= KIN_MAX) ? k0r : K, k1 = (P <= KIN_MAX) ? k1r : K;
     // Round 1: every load of the generation is issued before any value is used (one
     // memory round trip): hand words, first cloud point, push links, inbox payload rows
     // (waves 1..7); own state, own pbest cost, inbox tags / costs, gmin cells, sig (wave 0).
-    const double hw = hand_word<HPE_NT>(Hg);  // staged into LDS before the first barrier
+    // staged into LDS before the first barrier (after the argument batch: issued ahead of
+    // it, this load made the compiler wait for the first argument words alone)
+    const double hw = hand_word<HPE_NT>((const DevHand *)((const char *)Hg + z0));
     const DevHand *__restrict__ H = &sm.hand;
     sc.lap(4);
     const CloudGlobal cv = obs_cloud(o);
