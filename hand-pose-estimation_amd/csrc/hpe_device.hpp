@@ -753,11 +753,14 @@ __device__ __forceinline__ Pt load_pt(const CV &cv, int it) {
 // pre: the point of item threadIdx.x, loaded early by the caller (load_pt) so its
 // latency hides under FK.
 // gt: this thread's index among the NT threads searching for the particle.
+// stride / max_items (LDS cloud only): items gt, gt + stride, ... at most max_items of them
+// (the refine's correspondence search spreads its items unevenly over the waves).
 template <int NT, bool STORE_MATCH, class CV>
 __device__ __forceinline__ double search_align(const FkSm &f, const CV &cv,
                                                const DevHand *__restrict__ H,
                                                int32_t *__restrict__ match, Pt pre,
-                                               int gt = -1, int g_ts = BT_GENS) {
+                                               int gt = -1, int g_ts = BT_GENS,
+                                               int stride = NT, int max_items = 1 << 30) {
     if (gt < 0) gt = threadIdx.x;
     double acc = 0.0;
     const int h = gt & 1;
@@ -794,7 +797,9 @@ __device__ __forceinline__ double search_align(const FkSm &f, const CV &cv,
             q = qn;
         }
     } else {
-        for (int it = gt; it < 2 * cv.n; it += NT) item(it, it == gt ? pre : load_pt(cv, it));
+        int k = 0;
+        for (int it = gt; it < 2 * cv.n && k < max_items; it += stride, ++k)
+            item(it, it == gt ? pre : load_pt(cv, it));
     }
     return acc;
 }

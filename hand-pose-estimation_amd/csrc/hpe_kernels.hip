@@ -1359,7 +1359,18 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
                 const DepthG dgc = depth_issue_w0(rs.base, o, H);
                 const bool young = w >= HPE_SETPRIO_FROM;  // as in eval_block
                 if (young) __builtin_amdgcn_s_setprio(1);
-                double al = search_align<RF_NT, true>(rs.base, cv, H, match, load_pt(cv, t));
+                // (n <= 256) the items go where the SIMDs have room: waves 0..5 also run a
+                // gradient point's head below, two of them on SIMDs 0 and 1 each, one on
+                // SIMDs 2 and 3; so waves 4, 5 search nothing and waves 6, 7 two items
+                double al;
+                if (small) {
+                    const int f0 = (w < 4) ? 64 * w : (w >= 6) ? 256 + 128 * (w - 6) : 0;
+                    const int cnt = (w < 4) ? 1 : (w >= 6) ? 2 : 0;
+                    al = search_align<RF_NT, true>(rs.base, cv, H, match, load_pt(cv, f0 + l),
+                                                   f0 + l, BT_GENS, 64, cnt);
+                } else {
+                    al = search_align<RF_NT, true>(rs.base, cv, H, match, load_pt(cv, t));
+                }
                 if (young) __builtin_amdgcn_s_setprio(0);
                 double co = (t < 144) ? collide_term(rs.base, t, H) : 0.0;
                 const double dep = depth_finish(dgc, o, t < HPE_NS);
