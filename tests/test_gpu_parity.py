@@ -229,6 +229,31 @@ def test_refine_init_pose(oracle, ora_hand, gpu_hand, np_hand):
     np.testing.assert_allclose(x, x_ref, rtol=0, atol=1e-6)
 
 
+@pytest.mark.parametrize("npts", [256, 257, 1500])
+def test_refine_staged_cloud_sizes(oracle, ora_hand, gpu_hand, np_hand, npts):
+    """refine_init_pose on clouds staged in LDS at the sizes around its two paths: N <= 256
+    keeps each lane's matchIds in registers and spreads the correspondence items by SIMD
+    load; 256 < N <= 2048 runs the plain strided search and LDS alignment.  The frame keeps
+    the first npts foreground pixels of a rendered hand (no down-sampling)."""
+    import hpe
+    truth = hand_data.trajectory(2, seed=4)[1]
+    d = oracle_np.render_depth_mm(np_hand, truth)
+    fg = np.flatnonzero(d)
+    assert len(fg) > npts
+    d2 = np.zeros_like(d)
+    d2.flat[fg[:npts]] = d.flat[fg[:npts]]
+    obs, om = _obs_pair(oracle, gpu_hand, d2, downsample=False)
+    assert obs.n == npts
+    cf = hpe.costfunc(gpu_hand, om)
+    x0 = oracle_np.X0.copy()
+    x_ref, ev_ref = oracle.refine(ora_hand, obs, x0)
+    pso = hpe.PSO()
+    x = x0.copy()
+    pso.refine_init_pose(x, cf)
+    assert pso.last_refine_evals == ev_ref
+    np.testing.assert_allclose(x, x_ref, rtol=0, atol=1e-6)
+
+
 @pytest.mark.parametrize("mw", ["1", "0"])
 def test_refine_full_cloud(oracle, ora_hand, np_hand, mw, monkeypatch):
     """refine_init_pose on a full-resolution cloud (> 2048 points): the multi-workgroup
