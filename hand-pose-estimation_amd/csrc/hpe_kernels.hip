@@ -1307,7 +1307,7 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
     bool base_valid = false;
     const double e = 1e-5;  // cal_grad step (PSO.cpp:195)
     // clouds of at most FP_MAX points: each lane keeps its frozen points in registers
-    const bool small = !MW && STAGED && o.n <= FP_MAX;
+    const bool small = !MW && STAGED && o.n >= 1 && o.n <= FP_MAX;  // (N = 0: no point to clamp to)
     FrozenPts fpts;
     for (int blk = 0; blk < 2; ++blk) {
         const int lo = 3 * blk;  // start_idx (PSO.cpp:226-227); end_idx = lo + 2
