@@ -322,6 +322,31 @@ def test_edge_small_clouds(oracle, ora_hand, gpu_hand):
                                oracle.eval_costs(ora_hand, obs, oracle_np.X0[None]), rtol=RTOL)
 
 
+def test_edge_large_cloud(oracle, ora_hand, gpu_hand, np_hand):
+    """A frame whose foreground covers most of the image (a rendered hand in front of a
+    240 x 200 block at 60 cm: ~50k points, full resolution): costs and correspondences of
+    a particle batch against the oracle, and refine_init_pose (multi-workgroup form)."""
+    import hpe
+    truth = hand_data.trajectory(2, seed=4)[1]
+    d = oracle_np.render_depth_mm(np_hand, truth)
+    d = np.where(d > 0, d, 0).astype(np.float32)
+    blk = np.zeros_like(d)
+    blk[:, 60:260] = 600.0
+    d = np.where(d > 0, d, blk)
+    obs, om = _obs_pair(oracle, gpu_hand, d, downsample=False)
+    assert obs.n > 40000
+    cf = hpe.costfunc(gpu_hand, om)
+    th = np.vstack([truth, truth + 2, oracle_np.X0])
+    np.testing.assert_allclose(cf.cal_cost_batch(th), oracle.eval_costs(ora_hand, obs, th),
+                               rtol=RTOL)
+    x_ref, ev_ref = oracle.refine(ora_hand, obs, truth.copy())
+    pso = hpe.PSO()
+    x = truth.copy()
+    pso.refine_init_pose(x, cf)
+    assert pso.last_refine_evals == ev_ref
+    np.testing.assert_allclose(x, x_ref, rtol=0, atol=1e-6)
+
+
 def test_edge_empty_frame_optimisers(oracle, ora_hand, gpu_hand):
     """An all-background frame (N = 0): lambda = 48/0, so every cost is NaN as in the
     reference (costfunc.cpp:372); no pbest ever improves, gbest stays zeros (PSO.cpp:546),
