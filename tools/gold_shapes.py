@@ -6,7 +6,8 @@ failures then acceptance), and for a node budget K a shape per context (the prev
 last decision: a search's first round, "down", "up") is fitted by coordinate descent over
 all prefix-closed node sets of size K, minimising the speculated rounds.  Prints the round
 counts of each budget, the cross-validation over the sequences and the packed table entries
-gold_shape() takes.  CPU only.
+gold_shape() takes, then the per-context choice of 4 or 8 nodes by expected round time
+(GOLD_MIX).  CPU only.
 
 Usage: python tools/gold_shapes.py [refine|optimise] [frames] [seeds...]
 """
@@ -68,6 +69,20 @@ def rounds(policy, s):
         while pos < n and dec[start:pos] in T:
             pos += 1
     return r
+
+
+def rounds_time(policy, nodes, s, t4=0.71):
+    dec = s[:-1]
+    n = len(s) if s[-1] == "A" else len(dec)
+    pos, t = 0, 0.0
+    while pos < n:
+        c = "" if pos == 0 else dec[pos - 1]
+        T = policy[c]
+        t += t4 if nodes[c] <= 4 else 1.0
+        start = pos
+        while pos < n and dec[start:pos] in T:
+            pos += 1
+    return t
 
 
 def total(policy, logs):
@@ -136,12 +151,23 @@ def main():
         print(f"   {c:6d} {s}")
     bal = frozenset("".join(p) for k in range(3) for p in itertools.product("DU", repeat=k))
     print("balanced depth 3 (7 nodes):", total({c: bal for c in CTX}, allg))
+    fitted = {}
     for k in (4, 7, 8):
         pol, cur = fit(k, allg)
+        fitted[k] = pol
         xv = {s: total(pol, v) for s, v in logs.items()}
         print(f"{k} nodes: {cur} rounds, per sequence {xv}")
         for r in packed(pol):
             print("    " + r)
+    # round TIME: a round of <= 4 nodes runs one wave per SIMD, ~0.71 of an 8-node round
+    # (measured: two node waves on a SIMD take ~1.4x one); per context, 4 or 8 nodes
+    best = None
+    for choice in itertools.product((4, 8), repeat=3):
+        pol = {c: fitted[k][c] for c, k in zip(CTX, choice)}
+        t = sum(rounds_time(pol, {c: k for c, k in zip(CTX, choice)}, s) for s in allg)
+        print(f"time-weighted, nodes per context {dict(zip(('first', 'D', 'U'), choice))}: {t:.1f}")
+        best = min(best or (t, choice), (t, choice))
+    print("best:", best)
 
 
 if __name__ == "__main__":
