@@ -1117,12 +1117,13 @@ struct GoldShape {
 #define GOLD_4 3
 #define GOLD_OPT8 4  // pso_optimise's descent (tools/gold_shapes.py optimise)
 #define GOLD_MIX 5   // GOLD_8 after a search's start and a "down", GOLD_4 after an "up"
+#define GOLD_MIX2 6  // jointly fitted by round time: 8 nodes at a search's start, 4 after
 #ifndef HPE_GOLD_POLICY
 #define HPE_GOLD_POLICY GOLD_MIX  // refine_init_pose
 #endif
 template <int POL>
 __device__ __forceinline__ GoldShape gold_shape(int ctx) {
-    constexpr GoldShape T[18] = {
+    constexpr GoldShape T[21] = {
     // GOLD_BALANCED
     {7, 0x0043414240212000ull, 0xfffff531u, 0xfffff642u},  // first: '' 'D' 'U' 'DD' 'DU' 'UD' 'UU'
     {7, 0x0043414240212000ull, 0xfffff531u, 0xfffff642u},  // D: '' 'D' 'U' 'DD' 'DU' 'UD' 'UU'
@@ -1146,6 +1147,10 @@ __device__ __forceinline__ GoldShape gold_shape(int ctx) {
     // GOLD_MIX (4 nodes, one wave per SIMD, run a round in ~0.71 of an 8-node one)
     {8, 0xa080604340212000ull, 0xf76f5f31u, 0xfffff4f2u},  // first: '' 'D' 'U' 'DD' 'UU' 'DDD' 'DDDD' 'DDDDD'
     {8, 0x6043414240212000ull, 0xffff7531u, 0xfffff642u},  // D: '' 'D' 'U' 'DD' 'DU' 'UD' 'UU' 'DDD'
+    {4, 0x0000000040212000ull, 0xffffff31u, 0xfffffff2u},  // U: '' 'D' 'U' 'DD'
+    // GOLD_MIX2 (tools/gold_shapes.py, joint fit by round time)
+    {8, 0xa080604340212000ull, 0xf76f5f31u, 0xfffff4f2u},  // first: '' 'D' 'U' 'DD' 'UU' 'DDD' 'DDDD' 'DDDDD'
+    {4, 0x0000000040212000ull, 0xffffff31u, 0xfffffff2u},  // D: '' 'D' 'U' 'DD'
     {4, 0x0000000040212000ull, 0xffffff31u, 0xfffffff2u},  // U: '' 'D' 'U' 'DD'
     };
     return ctx == 0 ? T[3 * POL] : ctx == 1 ? T[3 * POL + 1] : T[3 * POL + 2];
