@@ -83,6 +83,10 @@ def parse():
     ap.add_argument("--resident", action="store_true",
                     help="preprocess every frame before timing (default: each step prepares "
                          "the next frame from host depth on the GPU, overlapped)")
+    ap.add_argument("--frames-per-graph", type=int, default=0,
+                    help="with --resident: track the frames through the offline sequence API "
+                         "(hpe_track_sequence_dev), this many frames per graph launch "
+                         "(default 0: one hpe_track_frame_dev graph per frame)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--seed", type=int, default=TRAJ_SEED, help="trajectory seed")
@@ -101,6 +105,9 @@ def parse():
                          "as .npy under this directory")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)
     a = ap.parse_args()
+    if a.frames_per_graph and not (a.resident and a.gpus == 1 and not a.dump):
+        ap.error("--frames-per-graph needs --resident, one GPU and no --dump "
+                 "(the per-frame exchange / dump sit between frames)")
     P, G, _ = CONFIGS[a.config]
     a.particles = a.particles or P
     a.generations = a.generations if a.generations is not None else G
@@ -383,21 +390,41 @@ def main():
         if rank == 0:
             np.save(os.path.join(args.dump, "raw0.npy"), raw[0])
             np.save(os.path.join(args.dump, "x0.npy"), state[:26].cpu().numpy())
+    K = args.frames_per_graph
+
+    def run_sequence(first, n):  # offline: frames first .. first+n-1, K per graph launch
+        ctx.track_sequence(P, refine, state.data_ptr(), first, n, K)
+
     if not args.resident:
         ctx.pipeline_begin(raw[0], True, ds)
-    for f in range(args.warmup):
-        step(f)
-        dump_state()
+    if K:
+        run_sequence(0, args.warmup)
+    else:
+        for f in range(args.warmup):
+            step(f)
+            dump_state()
     ctx.check(lib.hpe_sync(ctx.h))
     torch.cuda.synchronize()
     state0 = state.clone()  # the diagnostic passes below restart from here: same frames, same work
+    cold_ms = None
+    if K:  # capture the timed range's chunk graphs once (as the per-frame graph is in warmup)
+        tc = time.perf_counter()
+        run_sequence(args.warmup, args.steps)
+        ctx.check(lib.hpe_sync(ctx.h))
+        cold_ms = (time.perf_counter() - tc) / args.steps * 1e3
+        state.copy_(state0)
+        torch.cuda.synchronize()
     # timed region: graph-replayed frames, nothing else on the tracker stream
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     host_s = 0.0
-    for f in range(args.warmup, n_frames):
+    if K:
+        h0 = time.perf_counter()
+        run_sequence(args.warmup, args.steps)
+        host_s += time.perf_counter() - h0
+    for f in range(args.warmup, n_frames if not K else 0):
         h0 = time.perf_counter()
         step(f)
         host_s += time.perf_counter() - h0
@@ -423,13 +450,18 @@ def main():
     torch.cuda.synchronize()
     if not args.resident:
         ctx.pipeline_begin(raw[args.warmup], True, ds)
-    for k, f in enumerate(range(args.warmup, n_frames)):
+    if K:  # one event pair around the whole sequence
+        ev[0][0].record(ext)
+        run_sequence(args.warmup, args.steps)
+        ev[0][1].record(ext)
+    for k, f in enumerate(range(args.warmup, n_frames if not K else 0)):
         ev[k][0].record(ext)
         step(f)
         ev[k][1].record(ext)
     ctx.check(lib.hpe_sync(ctx.h))
     torch.cuda.synchronize()
-    frame_us = [a.elapsed_time(b) * 1e3 for a, b in ev]
+    frame_us = ([a.elapsed_time(b) * 1e3 for a, b in ev] if not K else
+                [ev[0][0].elapsed_time(ev[0][1]) * 1e3 / args.steps])
     # per-kernel durations: the same frames once more with every dispatch bracketed by
     # hipExtLaunchKernel start/stop events on the tracker stream the kernels run on
     # (direct launches; kernels are identical)
@@ -470,7 +502,9 @@ def main():
                            "min_us": min(frame_us), "max_us": max(frame_us),
                            "median_us": float(np.median(frame_us)),
                            "per_frame_us": [round(x, 1) for x in frame_us],
-                           "note": "one event pair per frame, a second pass over the frames"}
+                           "note": ("one event pair per frame, a second pass over the frames"
+                                    if not K else "one event pair around the whole sequence "
+                                    "(a second pass), per frame")}
     lib_path = hpe._lib.load()._name
 
     if rank == 0:
@@ -519,7 +553,11 @@ def main():
                                     "tracked frame = " + ("" if args.resident else
                                     "next_frame preprocessing (GPU, fused into the refine "
                                     "launch) + ") + "refine_init_pose + pso_evolve + "
-                                    "cal_cost(bestp)"),
+                                    "cal_cost(bestp)" + (
+                                        f"; frames resident in HBM, tracked by the offline "
+                                        f"sequence API, {K} frames per graph launch" if K
+                                        else "")),
+                       "frames_per_graph": K or 1,
                        "particles": P, "generations": G, "maxiter": G + 1,
                        "trajectory": (None if args.frames else
                                       {"seed": args.seed, "revert": TRAJ_REVERT,
@@ -542,6 +580,7 @@ def main():
             "refine_evals_per_frame": rev.value / max(ref_launches, 1),
             "kernels": prof,
             "host_us_per_step": host_s / args.steps * 1e6,
+            "cold_graphs_ms_per_step": cold_ms,
             "lib_sha256": lib_sha256(lib_path),
         }
         if world == 1 and not args.no_cpu_baseline:

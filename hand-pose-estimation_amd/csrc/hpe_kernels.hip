@@ -691,7 +691,8 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
                                                       DevObs *__restrict__ obs_out = nullptr,
                                                       int same_eval = 0,
                                                       unsigned long long *__restrict__ seq_dev = nullptr,
-                                                      unsigned long long *done_host = nullptr) {
+                                                      unsigned long long *done_host = nullptr,
+                                                      double *__restrict__ hist = nullptr) {
     constexpr int CH = 2048;  // generations staged per pass
     __shared__ Smem sm;
     __shared__ double gm[CH];
@@ -809,6 +810,7 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
             for (int d = 0; d < HPE_DOF; ++d) {
                 out[d] = r[d];
                 sw.gpos[d] = r[d];
+                if (hist) hist[d] = r[d];
             }
         }
         if (TAIL && !same_eval) {  // the tail below evaluates cal_cost(bestp)
@@ -837,9 +839,13 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
         if (t < HPE_DOF) {
             out[t] = bp;
             sw.gpos[t] = bp;
+            if (hist) hist[t] = bp;
         }
     }
-    if (t == 0) out[HPE_DOF] = gcost;
+    if (t == 0) {
+        out[HPE_DOF] = gcost;
+        if (hist) hist[HPE_DOF] = gcost;
+    }
     for (int c = t; c < (G + 1) * GMIN_SHARDS; c += HPE_NT) sw.gmin[(size_t)c * GMIN_STRIDE] = ~0ull;
     if (TAIL) {
         if (obs_out && t < (int)(sizeof(DevObs) / 8)) ((unsigned long long *)obs_out)[t] = obs_word;
@@ -850,7 +856,10 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
         const Pt pre = load_pt(cv, t);
         __syncthreads();
         const double c = eval_block<EV_COST, HPE_NT>(sm, o, cv, &sm.hand, nullptr, pre);
-        if (t == 0) out[HPE_DOF] = c;
+        if (t == 0) {
+            out[HPE_DOF] = c;
+            if (hist) hist[HPE_DOF] = c;
+        }
     }
 }
 

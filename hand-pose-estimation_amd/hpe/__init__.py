@@ -112,6 +112,15 @@ class Context:
                                                 C.c_void_p(d_state_ptr),
                                                 ptr(nd, C.c_float) if nd is not None else None))
 
+    def track_sequence(self, num_p, refine, d_state_ptr, first_slot, n, frames_per_graph=0,
+                       d_hist_ptr=None):
+        """Track resident frames first_slot .. first_slot+n-1 in order (test_full's loop),
+        frames_per_graph of them per graph launch; frame f's {bestp, cost} to d_hist_ptr +
+        27 f (device, optional).  Asynchronous on the context stream."""
+        self.check(self.lib.hpe_track_sequence_dev(
+            self._h, int(num_p), int(refine), C.c_void_p(d_state_ptr), int(first_slot), int(n),
+            int(frames_per_graph), C.c_void_p(d_hist_ptr) if d_hist_ptr else None))
+
     def frame_readback(self, slot):
         depth = np.zeros((IMG_H, IMG_W)); dt = np.zeros((IMG_H, IMG_W), dtype=np.float32)
         cloud = np.zeros((IMG_H * IMG_W, 3)); n = C.c_int32(0)

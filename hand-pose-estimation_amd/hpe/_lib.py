@@ -65,6 +65,8 @@ SIGNATURES = {
     "hpe_refine_init_pose": (C.c_int, [C.c_void_p, dp, ip]),
     "hpe_track_frame": (C.c_int, [C.c_void_p, C.c_int, C.c_int, dp, dp]),
     "hpe_track_frame_dev": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
+    "hpe_track_sequence_dev": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int,
+                                         C.c_int, C.c_int, C.c_void_p]),
     "hpe_profile_enable": (C.c_int, [C.c_void_p, C.c_int]),
     "hpe_profile_read": (C.c_int, [C.c_void_p, ip, dp, dp, dp]),
     "hpe_profile_read_kernel": (C.c_int, [C.c_void_p, C.c_int, ip, dp, dp, dp]),

@@ -176,6 +176,19 @@ int hpe_track_frame(hpe_ctx *ctx, int num_p, int refine, double x0_inout[26],
  * hpe_stream(ctx): no host synchronisation. */
 int hpe_track_frame_dev(hpe_ctx *ctx, int num_p, int refine, double *d_state);
 
+/* Offline tracking of a recorded sequence: test_full's loop (testmodel.cpp:117-139) over
+ * frames already resident in HBM, slots first_slot .. first_slot+n-1 (hpe_store_frame /
+ * hpe_prepare_frame), each tracked exactly like hpe_track_frame_dev on its own slot and
+ * d_state carried from frame to frame.  Frames are captured frames_per_graph at a time
+ * into one graph (0: HPE_SEQ_CHUNK), so the graph-to-graph gap is paid once per chunk;
+ * captured chunks are cached per slot range.  d_hist (device, optional): n x 27 doubles,
+ * frame f's {bestp, cost}.  Asynchronous on hpe_stream(ctx); the last frame is the
+ * selected one afterwards, and a later hpe_prepare_frame waits for the sequence. */
+#define HPE_SEQ_CHUNK 8
+#define HPE_SEQ_MAX_CHUNK 32
+int hpe_track_sequence_dev(hpe_ctx *ctx, int num_p, int refine, double *d_state,
+                           int first_slot, int n, int frames_per_graph, double *d_hist);
+
 /* Pipelined tracking: test_full's loop (testmodel.cpp:117-139) with next_frame
  * (observedmodel.cpp:420-430) of frame f+1 running INSIDE frame f's refine launch, on CUs
  * the single-workgroup refine leaves idle: one stream, one replayed graph per frame.

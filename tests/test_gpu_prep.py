@@ -124,3 +124,58 @@ def test_pipelined_tracking_like_oracle(gh, oracle, ora_hand, np_hand, downsampl
         cr = oracle.cal_cost(ora_hand, obs, x_ref)
         np.testing.assert_allclose(out[:26], x_ref, rtol=0, atol=1e-6)
         assert abs(out[26] - cr) <= 1e-8 * abs(cr)
+
+
+def test_sequence_tracking_like_oracle_and_per_frame(gh, oracle, ora_hand, np_hand):
+    """hpe_track_sequence_dev (offline test_full loop over resident frames, several frames
+    per graph launch): every frame's {bestp, cost} equals the oracle's loop, and equals
+    hpe_track_frame_dev frame by frame bit for bit, for chunks of 1, 3 (ragged: 3 + 3 + 1)
+    and 8 frames; a second call replays the cached graphs to the same bits."""
+    import ctypes as C
+    import hpe
+    import torch
+    n, P, maxiter, s0 = 7, 32, 6, 400
+    poses = hand_data.trajectory(n, seed=23)
+    depth = [oracle_np.render_depth_mm(np_hand, th) for th in poses]
+    ub, lb, sd = oracle_np.reference_bounds()
+    pso = hpe.PSO()
+    pso.set_pso_params(ub, lb, sd, 0.7298, 1.49618, 1.49618, maxiter, 1e-8, 1e-8)
+    pso._push(gh.ctx)
+    for f in range(n):
+        gh.ctx.prepare_frame(s0 + f, depth[f])
+    rt = gh.ctx.lib
+    # per-frame reference on the GPU: select + hpe_track_frame_dev
+    st = torch.zeros(27, dtype=torch.float64, device="cuda:0")
+    st[:26] = torch.from_numpy(oracle_np.X0)
+    per_frame = []
+    for f in range(n):
+        gh.ctx.select_frame(s0 + f)
+        gh.ctx.check(rt.hpe_track_frame_dev(gh.ctx.h, P, 1, C.c_void_p(st.data_ptr())))
+        gh.ctx.check(rt.hpe_sync(gh.ctx.h))
+        per_frame.append(st.cpu().numpy().copy())
+    per_frame = np.array(per_frame)
+    # the oracle's test_full loop
+    x_ref = oracle_np.X0.copy()
+    for f in range(n):
+        obs = oracle.preprocess(depth[f])
+        x_ref, _ = oracle.refine(ora_hand, obs, x_ref)
+        x_ref, _, _ = oracle.pso_evolve(ora_hand, obs, x_ref, P, maxiter, lb, ub, sd)
+        cr = oracle.cal_cost(ora_hand, obs, x_ref)
+        np.testing.assert_allclose(per_frame[f, :26], x_ref, rtol=0, atol=1e-6)
+        assert abs(per_frame[f, 26] - cr) <= 1e-8 * abs(cr)
+    for K in (1, 3, 8, 3):  # the last: cached graphs
+        st[:26] = torch.from_numpy(oracle_np.X0)
+        st[26] = 0.0
+        hist = torch.full((n, 27), float("nan"), dtype=torch.float64, device="cuda:0")
+        torch.cuda.synchronize()
+        gh.ctx.track_sequence(P, 1, st.data_ptr(), s0, n, K, hist.data_ptr())
+        gh.ctx.check(rt.hpe_sync(gh.ctx.h))
+        h = hist.cpu().numpy()
+        assert np.array_equal(h, per_frame), K
+        assert np.array_equal(st.cpu().numpy(), per_frame[-1]), K
+    # argument errors
+    bad = rt.hpe_track_sequence_dev
+    assert bad(gh.ctx.h, P, 1, C.c_void_p(st.data_ptr()), s0, 0, 0, None) == hpe._lib.HPE_E_ARG
+    assert bad(gh.ctx.h, P, 1, C.c_void_p(st.data_ptr()), 4095, 2, 0, None) == hpe._lib.HPE_E_ARG
+    assert bad(gh.ctx.h, P, 1, C.c_void_p(st.data_ptr()), s0, n, 33, None) == hpe._lib.HPE_E_ARG
+    assert bad(gh.ctx.h, P, 1, None, s0, n, 0, None) == hpe._lib.HPE_E_ARG
