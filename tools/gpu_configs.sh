@@ -9,4 +9,5 @@ timeout -k 10 300 python bench.py --steps 400 --warmup 1 --no-cpu-baseline > $O/
 timeout -k 10 300 python bench.py --config p4096 --no-cpu-baseline > $O/p4096.log 2>&1 && \
 timeout -k 10 300 python bench.py --config p32 --no-cpu-baseline > $O/p32.log 2>&1 && \
 timeout -k 10 300 python bench.py --config subswarm8 --no-cpu-baseline > $O/subswarm1.log 2>&1 && \
-timeout -k 10 300 python bench.py --resident --no-cpu-baseline > $O/resident.log 2>&1
+timeout -k 10 300 python bench.py --resident --no-cpu-baseline > $O/resident.log 2>&1 && \
+timeout -k 10 300 python bench.py --resident --frames-per-graph 8 --no-cpu-baseline > $O/resident_seq8.log 2>&1
