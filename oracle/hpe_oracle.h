@@ -88,6 +88,8 @@ int ora_pso_evolve(const ora_hand *h, const ora_obs *o, const double x0[26], int
                    double *bestcost, ora_pso_trace *trace, int nthreads);
 
 int ora_refine_init_pose(const ora_hand *h, const ora_obs *o, double x0[26]);
+/* test instrumentation: smallest relative decision margin of the last refine */
+double ora_refine_last_margin(void);
 /* diagnostic: log every Goldstein search's decisions into buf (see hpe_oracle.c) */
 void ora_set_gold_log(uint64_t *buf, int cap);
 int ora_gold_log_count(void);

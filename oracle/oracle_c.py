@@ -87,6 +87,7 @@ class Oracle:
         L.ora_pso_optimise.restype = C.c_int
         L.ora_refine_init_pose.argtypes = [C.POINTER(OraHand), C.POINTER(OraObs), dp]
         L.ora_refine_init_pose.restype = C.c_int
+        L.ora_refine_last_margin.restype = C.c_double
         L.ora_gnd_truth_err.argtypes = [dp, dp, C.c_int, C.c_int]
         L.ora_gnd_truth_err.restype = C.c_double
         L.ora_dist_transform.argtypes = [dp, fp]
@@ -192,6 +193,11 @@ class Oracle:
         x = np.array(x0, dtype=np.float64)
         ev = self.lib.ora_refine_init_pose(C.byref(h), C.byref(obs.s), _p(x, C.c_double))
         return x, ev
+
+    def refine_last_margin(self):
+        """The smallest relative decision margin of the last refine() (test
+        instrumentation, hpe_oracle.c margin_note)."""
+        return float(self.lib.ora_refine_last_margin())
 
     # ---- evaluation
     def gnd_truth_err(self, hand_joints, gnd_truth, frame):

@@ -72,6 +72,10 @@ def test_pso_refine_golden(oracle, ora_hand, frame):
     # central differences (eps 1e-5) turn last-ulp cost differences (numpy's pairwise sum
     # vs Armadillo's 2-accumulator order) into ~1e-8 gradient differences
     np.testing.assert_allclose(x, g["refined"], rtol=0, atol=1e-7)
+    # the decision-margin instrumentation the sequence tests rely on: refine took at least
+    # one Goldstein test, so its smallest margin is finite and non-negative
+    m = oracle.refine_last_margin()
+    assert 0.0 <= m < float("inf")
 
 
 def test_pso_optimise_golden(oracle, ora_hand, frame):
