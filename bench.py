@@ -187,9 +187,15 @@ def cpu_baseline(args, recorded=None):
 
     affinity = len(os.sched_getaffinity(0))
     quota = cgroup_cpu_quota()
-    legs = {"affinity": leg(affinity, args.cpu_seconds, 4096)}
+    skipped = None
     if quota and quota < affinity:
-        legs["cgroup_quota"] = leg(quota, args.cpu_seconds, 4096)
+        # more OpenMP threads than the cgroup grants stall at every barrier (measured on
+        # the box: 256 affinity threads under a 16-CPU quota ran 0.26 FPS): time the quota
+        legs = {"cgroup_quota": leg(quota, args.cpu_seconds, 4096)}
+        skipped = (f"affinity leg ({affinity} threads) not run: the cgroup quota grants "
+                   f"{quota} CPUs, so {affinity} OpenMP threads would be oversubscribed")
+    else:
+        legs = {"affinity": leg(affinity, args.cpu_seconds, 4096)}
     best = max(legs.values(), key=lambda r: r["value"])
     one = leg(1, args.cpu_seconds / 3, 1024)
     out = {"value": best["value"], "unit": "particle-evals/s", "cores": best["threads"],
@@ -198,7 +204,7 @@ def cpu_baseline(args, recorded=None):
                       f"N={best['cloud_points']}, refine={'off' if args.no_refine else 'on'}) "
                       f"of the same synthetic sequence in {best['seconds']:.1f} s, "
                       f"oracle/hpe_oracle.c with {best['threads']} OpenMP threads"),
-           "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+           "affinity_cpus": affinity, "cgroup_cpu_quota": quota, "skipped_leg": skipped,
            "legs": {k: {kk: v[kk] for kk in ("threads", "value", "tracked_fps", "frames")}
                     for k, v in legs.items()},
            "one_thread": {"value": one["value"], "tracked_fps": one["tracked_fps"],
@@ -255,6 +261,64 @@ def roofline_entry(kernel, prof, evals_per_launch, n_pts, lib_path, P):
 
 
 # ------------------------------------------------------------------------- stub ranks
+def device_identity(local):
+    """This rank's GPU: PCI domain:bus:device and UUID from the HIP device properties."""
+    import torch
+    pr = torch.cuda.get_device_properties(local)
+    pci = ":".join(str(getattr(pr, k, "?")) for k in ("pci_domain_id", "pci_bus_id",
+                                                        "pci_device_id"))
+    return {"pci": pci, "uuid": str(getattr(pr, "uuid", "")), "name": pr.name,
+            "local_rank": local}
+
+
+def rccl_version():
+    import torch
+    try:
+        v = torch.cuda.nccl.version()
+        return ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
+    except Exception as e:  # noqa: BLE001
+        return f"unavailable ({type(e).__name__})"
+
+
+def rank_report(args, world, rank, el, final, dev, ident):
+    """Self-verification of a multi-rank run (every rank calls it): the world size from the
+    process group, the collective library's version, each rank's device (distinct unless
+    --same-device), min / max of the ranks' times, and every rank's final 27-double state
+    identical (all adopted the same best at the last exchange).  Returns (max time over
+    ranks, the report); raises SystemExit on a failed check."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    ts = torch.zeros(world, dtype=torch.float64, device=dev)
+    dist.all_gather_into_tensor(ts, t)
+    el_all = ts.cpu().numpy()
+    fs = torch.from_numpy(np.ascontiguousarray(final, dtype=np.float64)).to(dev)
+    fa = torch.zeros(world * 27, dtype=torch.float64, device=dev)
+    dist.all_gather_into_tensor(fa, fs)
+    fa = fa.cpu().numpy().reshape(world, 27)
+    same_state = bool(np.all((fa == fa[0]) | (np.isnan(fa) & np.isnan(fa[0]))))
+    ids = [None] * world
+    dist.all_gather_object(ids, ident)
+    keys = [d["pci"] + "/" + d["uuid"] for d in ids]
+    distinct = len(set(keys)) == world
+    rep = {"world_size_pg": dist.get_world_size(), "backend": dist.get_backend(),
+           "rccl_version": rccl_version() if dist.get_backend() == "nccl" else None,
+           "devices": ids, "devices_distinct": distinct,
+           "same_device_mode": bool(args.same_device),
+           "ms_per_step_min": float(el_all.min()) / args.steps * 1e3,
+           "ms_per_step_max": float(el_all.max()) / args.steps * 1e3,
+           "final_state_identical": same_state}
+    if rep["world_size_pg"] != world:
+        raise SystemExit(f"rank {rank}: process group of {rep['world_size_pg']}, WORLD_SIZE {world}")
+    if not same_state:
+        raise SystemExit(f"rank {rank}: the ranks' final states differ after the exchange")
+    if not distinct and not args.same_device:
+        raise SystemExit(f"rank {rank}: two ranks share a device ({keys}); --same-device "
+                         "rehearses several ranks on one GPU")
+    return float(el_all.max()), rep
+
+
 def stub_main(args, world, rank):
     """CPU rehearsal of the multi-rank path: gloo, each rank a stub tracker state whose
     cost depends on the rank, the same per-frame exchange, barrier + max-over-ranks
@@ -283,13 +347,15 @@ def stub_main(args, world, rank):
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    t = torch.tensor([el], dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ranks = None
+    if world > 1:  # stub ranks: the host CPU each, told apart by rank
+        el, ranks = rank_report(args, world, rank, el, state.numpy(), "cpu",
+                                {"pci": "cpu", "uuid": f"stub-rank{rank}", "name": "stub",
+                                 "local_rank": rank})
     if rank == 0:
-        print(json.dumps({"metric": "stub exchange", "value": args.steps * world / float(t[0]),
+        print(json.dumps({"metric": "stub exchange", "value": args.steps * world / el,
                           "unit": "frames/s", "n_gpus": world, "steps": args.steps,
-                          "warmup": args.warmup, "stub": True,
+                          "warmup": args.warmup, "stub": True, "ranks": ranks,
                           "winner_rank": int(state[0]), "winner_cost": float(state[26])}),
               flush=True)
     if world > 1:
@@ -361,7 +427,8 @@ def main():
     gathered_host = torch.zeros(world * 27, dtype=torch.float64)
     refine = 0 if args.no_refine else 1
 
-    def step(f):
+    def step(f, ex=None):
+        """One tracked frame; ex (diagnostic pass): gets the exchange's time in us."""
         if args.resident:
             ctx.select_frame(f)
             ctx.check(lib.hpe_track_frame_dev(ctx.h, P, refine, C.c_void_p(state.data_ptr())))
@@ -370,12 +437,21 @@ def main():
         if world > 1 and args.backend == "nccl":
             # best-of-N exchange on the tracker's own stream (no host sync)
             with torch.cuda.stream(ext):
+                if ex is not None:
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(ext)
                 exchange_best(state, gathered)
+                if ex is not None:
+                    e1.record(ext)
+                    ex.append((e0, e1))
         elif world > 1:  # gloo: through host memory (rehearsal mode, synchronous)
             ctx.check(lib.hpe_sync(ctx.h))
+            h0 = time.perf_counter()
             hs = state.cpu()
             exchange_best(hs, gathered_host)
             state.copy_(hs)
+            if ex is not None:
+                ex.append((time.perf_counter() - h0) * 1e6)
 
     dumped = []
 
@@ -434,12 +510,11 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64,
-                         device=f"cuda:{local}" if args.backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    ranks = None
     final = state.cpu().numpy()
+    if world > 1:
+        dev = f"cuda:{local}" if args.backend == "nccl" else "cpu"
+        el, ranks = rank_report(args, world, rank, el, final, dev, device_identity(local))
     if args.dump:
         np.save(os.path.join(args.dump, f"states_rank{rank}.npy"), np.array(dumped))
     # per-frame device time: the same frames again with one event pair per frame on the
@@ -454,14 +529,23 @@ def main():
         ev[0][0].record(ext)
         run_sequence(args.warmup, args.steps)
         ev[0][1].record(ext)
+    ex = []  # the per-frame exchange (N > 1): event pairs around it on the tracker stream
     for k, f in enumerate(range(args.warmup, n_frames if not K else 0)):
         ev[k][0].record(ext)
-        step(f)
+        step(f, ex if world > 1 else None)
         ev[k][1].record(ext)
     ctx.check(lib.hpe_sync(ctx.h))
     torch.cuda.synchronize()
     frame_us = ([a.elapsed_time(b) * 1e3 for a, b in ev] if not K else
                 [ev[0][0].elapsed_time(ev[0][1]) * 1e3 / args.steps])
+    ex_us = [x if isinstance(x, float) else x[0].elapsed_time(x[1]) * 1e3 for x in ex]
+    if ranks is not None and ex_us:
+        ranks["exchange_us"] = {
+            "mean": float(np.mean(ex_us)), "median": float(np.median(ex_us)),
+            "max": float(np.max(ex_us)), "frames": len(ex_us),
+            "note": ("rank 0: events around the all-gather + pick on the tracker stream (the "
+                     "wait for the other ranks included), second pass" if args.backend == "nccl"
+                     else "rank 0: host wall time of the gloo exchange, second pass")}
     # per-kernel durations: the same frames once more with every dispatch bracketed by
     # hipExtLaunchKernel start/stop events on the tracker stream the kernels run on
     # (direct launches; kernels are identical)
@@ -581,6 +665,7 @@ def main():
             "kernels": prof,
             "host_us_per_step": host_s / args.steps * 1e6,
             "cold_graphs_ms_per_step": cold_ms,
+            "ranks": ranks,
             "lib_sha256": lib_sha256(lib_path),
         }
         if world == 1 and not args.no_cpu_baseline:

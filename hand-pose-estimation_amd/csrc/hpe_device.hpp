@@ -533,6 +533,102 @@ __device__ __forceinline__ double block_sum1(double (*red)[4], double v) {
     return r;
 }
 
+// ---------------------------------------------------------------- rigid refine FK
+// refine_init_pose moves only theta0..5 (PSO.cpp:225-227): the 20 digit angles are fixed
+// for the whole call.  Every joint is u + Rg * x with Rg = Rz(theta0 + 180) Ry(theta1)
+// Rx(theta2) (fingermodel.cpp:165-180) and x depending on the digit angles only
+// (T00 * Tgb is the first factor of every chain, fingermodel.cpp:289), and a sphere is an
+// affine combination of two joints, so
+//     S_k = negate_yz(Rg * q_k + u),   q_k = the hand-frame centre,
+// with q_k = the reference FK at theta0 = -180, theta1..5 = 0 (Tgb = I, u = 0 exactly:
+// sincos(0) = (0, 1)) with y, z un-negated.  The self-collision penalty depends on the
+// pairwise distances only, so it is a constant C of the call.  A refine node then costs
+// three sincos and a 3x3 rotation (block 2, translation only: P_k + u with P_k = Rg * q_k
+// of the block's fixed rotation) instead of the 5-digit DH chains.  Not the reference's
+// operation order: spheres agree with the chain to ~1e-14 cm and costs to ~1e-15
+// relative (DESIGN.md §2 states the tolerance; HPE_REFINE_EXACT=1 selects the chain).
+struct __align__(16) RigidSm {
+    double q[HPE_NS][3];  // hand-frame centres
+    double P[HPE_NS][3];  // Rg(x0) q_k, block 2
+    double C;             // self_collision_penalty (costfunc.cpp:130-197), rigid-invariant
+};
+
+// Row r of Rg from the three angles' sines / cosines: the operations fk_wave_t applies
+// to row r (Rz, then * Ry, then * Rx), zero terms included.
+__device__ __forceinline__ void rigid_row(int r, double sz, double cz, double sy, double cy,
+                                          double sx, double cx, double &g0, double &g1,
+                                          double &g2) {
+    double z0, z1, z2;
+    if (r == 0) { z0 = cz; z1 = -sz; z2 = 0; }
+    else if (r == 1) { z0 = sz; z1 = cz; z2 = 0; }
+    else { z0 = 0; z1 = 0; z2 = 1; }
+    const double q0 = z0 * cy + z2 * (-sy);
+    const double q1 = z1;
+    const double q2 = z0 * sy + z2 * cy;
+    g0 = q0;
+    g1 = q1 * cx + q2 * sx;
+    g2 = q1 * (-sx) + q2 * cx;
+}
+
+// Spheres of the refine node whose theta[l] is thl (lanes 0..25; lanes 0..2 and 3..5 are
+// read, the digits are in R.q) into f.S / f.Sp; lane l < 48 keeps its centre in own.
+// MODE 0: rotation block (trig on lanes 0..2, Rg rows, Rg q + u); MODE 1: translation
+// block (P + u); MODE 2: store P = Rg q into Pout (u ignored, f untouched).
+enum RigidMode { RG_ROT = 0, RG_TRANS = 1, RG_STORE_P = 2 };
+template <int MODE, bool OUTLINE_TRIG = true>
+__device__ __forceinline__ void rigid_wave(FkSm &f, const RigidSm &R, double thl,
+                                           SphXYZ *own = nullptr, double (*Pout)[3] = nullptr) {
+    const int l = threadIdx.x & 63;
+    const int sl = l < HPE_NS ? l : HPE_NS - 1;
+    const double a0 = MODE == RG_TRANS ? R.P[sl][0] : R.q[sl][0];
+    const double a1 = MODE == RG_TRANS ? R.P[sl][1] : R.q[sl][1];
+    const double a2 = MODE == RG_TRANS ? R.P[sl][2] : R.q[sl][2];
+    double v[3];
+    const double u[3] = {readlane_f64(thl, 3), readlane_f64(thl, 4), readlane_f64(thl, 5)};
+    if (MODE == RG_TRANS) {
+        v[0] = a0 + u[0];
+        v[1] = a1 + u[1];
+        v[2] = a2 + u[2];
+    } else {
+        double s = 0.0, c = 1.0;
+        if (l < 3) {  // TWS, ANG, ROT (fingermodel.cpp:91-93)
+            const double a = deg2rad(l == 0 ? thl + 180 : thl);
+            if (OUTLINE_TRIG) {
+                const SinCos r = sincos_outline(a);
+                s = r.s;
+                c = r.c;
+            } else {
+                sincos(a, &s, &c);
+            }
+        }
+        const double sz = readlane_f64(s, 0), cz = readlane_f64(c, 0);
+        const double sy = readlane_f64(s, 1), cy = readlane_f64(c, 1);
+        const double sx = readlane_f64(s, 2), cx = readlane_f64(c, 2);
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            double g0, g1, g2;
+            rigid_row(r, sz, cz, sy, cy, sx, cx, g0, g1, g2);
+            const double p = (g0 * a0 + g1 * a1) + g2 * a2;
+            if (MODE == RG_STORE_P) {
+                if (l < HPE_NS) Pout[l][r] = p;
+            }
+            v[r] = p + u[r];
+        }
+        if (MODE == RG_STORE_P) return;
+    }
+    v[1] = v[1] * -1;  // handmodel.cpp:288
+    v[2] = v[2] * -1;
+    if (l < HPE_NS) {
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            f.S[l][r] = v[r];
+            f.Sp[r][l] = (float)v[r];
+        }
+    }
+    if (own) *own = (l < HPE_NS) ? SphXYZ{v[0], v[1], v[2]} : SphXYZ{0.0, 0.0, 0.0};
+    wave_sync();
+}
+
 // ---------------------------------------------------------------- cost terms
 // depth_penalty term of sphere i (costfunc.cpp:249-300); S is un-negated on the fly.
 // Two halves, so that the gathers' L2 round trip overlaps the caller's other work:
@@ -1061,6 +1157,19 @@ __device__ __forceinline__ FrozenHead frozen_head(FkSm &f, const DevObs &o,
     }
     r.co = collide_value(cp[0], rt[0]) + collide_value(cp[1], rt[1]) +
            ((l < 16) ? collide_value(cp[2], rt[2]) : 0.0);
+    return r;
+}
+// frozen_head of the rigid refine (rigid_wave above): the collision is the constant R.C,
+// added by the caller after the sum.
+template <int MODE>
+__device__ __forceinline__ FrozenHead rigid_head(FkSm &f, const DevObs &o,
+                                                 const DevHand *__restrict__ H,
+                                                 const RigidSm &R, double thl) {
+    SphXYZ own;
+    rigid_wave<MODE>(f, R, thl, &own);
+    FrozenHead r;
+    r.dg = depth_issue_at(own, threadIdx.x & 63, o, H);
+    r.co = 0.0;
     return r;
 }
 template <class CV>

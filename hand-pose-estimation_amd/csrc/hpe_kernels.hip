@@ -889,6 +889,7 @@ struct __align__(16) RefineSm {
     double f[RF_NW];
     double fg[RF_NW];  // the gradient points' costs (k_refine, single-workgroup form)
     FkX X;  // rotation-only joint terms of x0 (refine block 2: translation steps)
+    RigidSm rg;  // hand-frame centres, block 2's rotated centres, collision (rigid refine)
     unsigned ts_n;  // diagnostic build: refine timeline entries written
 };
 
@@ -917,8 +918,8 @@ __device__ __forceinline__ void gold_down(double a, double &b, double &alpha) {
 #define MW_SPIN_MAX (1 << 21)
 static_assert(MW_MAX_Q % MW_DONE_SHARDS == 0, "helpers split evenly over the shards");
 
-__device__ __forceinline__ bool mw_wait_geq(unsigned *p, unsigned v) {
-    for (int i = 0; i < MW_SPIN_MAX; ++i) {
+__device__ __forceinline__ bool mw_wait_geq(unsigned *p, unsigned v, int spin) {
+    for (int i = 0; i < spin; ++i) {
         if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= v) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             return true;
@@ -926,6 +927,13 @@ __device__ __forceinline__ bool mw_wait_geq(unsigned *p, unsigned v) {
         __builtin_amdgcn_s_sleep(2);
     }
     return false;
+}
+
+// A hand-off timed out: flag it on the device (hpe_sync) and in pinned host memory (the
+// next tracking call), both plain stores of 1.
+__device__ __forceinline__ void mw_fail(const DevMw &mw) {
+    __hip_atomic_store(mw.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (mw.err_host) __hip_atomic_store(mw.err_host, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 struct MwLeader {
@@ -961,8 +969,9 @@ __device__ void mw_collect(MwLeader &ml, int *flag) {
     if (threadIdx.x == 0) {
         bool ok = !ml.failed;
         const unsigned want = ml.k * (unsigned)(ml.mw.Q / MW_DONE_SHARDS);
-        for (int s = 0; s < MW_DONE_SHARDS && ok; ++s) ok = mw_wait_geq(&ml.mw.ctr[32 * (1 + s)], want);
-        if (!ok) atomicExch(ml.mw.err, 1);
+        for (int s = 0; s < MW_DONE_SHARDS && ok; ++s)
+            ok = mw_wait_geq(&ml.mw.ctr[32 * (1 + s)], want, ml.mw.spin);
+        if (!ok) mw_fail(ml.mw);
         *flag = ok ? 1 : 0;
     }
     __syncthreads();
@@ -978,17 +987,26 @@ __device__ __forceinline__ double mw_sum(const MwLeader &ml, int w) {
 
 // rs.f[w] = cal_cost2(rs.w[w].th, matchId, false) for w < nn; each wave has written its
 // own rs.w[w].th.  Ends with a workgroup barrier.
-template <bool MW, class CV>
+// RIGID: the nodes' spheres by rigid_wave (rblk 0: rotation block, 1: translation block),
+// the collision the constant rs.rg.C.
+template <bool MW, bool RIGID = false, class CV>
 __device__ __forceinline__ void eval_nodes(RefineSm &rs, int nn, const DevObs &o, const CV &cv,
                                            const DevHand *__restrict__ H,
                                            const int32_t *__restrict__ match, FkX *Xt,
                                            MwLeader *ml, int *flag, const double *thr = nullptr,
-                                           const FrozenPts *fp = nullptr) {
+                                           const FrozenPts *fp = nullptr, int rblk = 0) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     if (!MW) {
         if (w < nn) {
             wave_sync();
-            const double f = eval_wave_frozen<true>(rs.w[w], o, cv, H, match, Xt, thr, fp);
+            double f;
+            if (RIGID) {
+                const FrozenHead hd = rblk ? rigid_head<RG_TRANS>(rs.w[w], o, H, rs.rg, *thr)
+                                           : rigid_head<RG_ROT>(rs.w[w], o, H, rs.rg, *thr);
+                f = frozen_tail(rs.w[w], o, cv, H, match, hd, fp) + rs.rg.C;
+            } else {
+                f = eval_wave_frozen<true>(rs.w[w], o, cv, H, match, Xt, thr, fp);
+            }
             if (l == 0) rs.f[w] = f;
         }
         REF_TS(rs.ts_n, 9);  // wave 0's node done
@@ -999,23 +1017,32 @@ __device__ __forceinline__ void eval_nodes(RefineSm &rs, int nn, const DevObs &o
     mw_publish(*ml, rs, MW_JOB_FROZEN, nn);
     double dep = 0.0, co = 0.0;
     if (w < nn) {  // depth + collision here while the helpers align
-        if (Xt) fk_wave_t<FK_TRANSLATE>(rs.w[w], H, Xt);
-        else fk_wave(rs.w[w], H);
-        dep = (l < HPE_NS) ? depth_term(rs.w[w], l, o, H) : 0.0;
-        co = collide_term(rs.w[w], l, H) + collide_term(rs.w[w], l + 64, H) +
-             ((l < 16) ? collide_term(rs.w[w], l + 128, H) : 0.0);
-        wave_sum2(dep, co);
+        if (RIGID) {
+            const double thl = rs.w[w].th[l < HPE_DOF ? l : 0];
+            if (rblk) rigid_wave<RG_TRANS>(rs.w[w], rs.rg, thl);
+            else rigid_wave<RG_ROT>(rs.w[w], rs.rg, thl);
+            dep = (l < HPE_NS) ? depth_term(rs.w[w], l, o, H) : 0.0;
+            dep = wave_sum(dep);
+        } else {
+            if (Xt) fk_wave_t<FK_TRANSLATE>(rs.w[w], H, Xt);
+            else fk_wave(rs.w[w], H);
+            dep = (l < HPE_NS) ? depth_term(rs.w[w], l, o, H) : 0.0;
+            co = collide_term(rs.w[w], l, H) + collide_term(rs.w[w], l + 64, H) +
+                 ((l < 16) ? collide_term(rs.w[w], l + 128, H) : 0.0);
+            wave_sum2(dep, co);
+        }
     }
     mw_collect(*ml, flag);
     if (w < nn) {
         const double al = mw_sum(*ml, w);
-        if (l == 0) rs.f[w] = ml->failed ? __builtin_nan("") : (al * o.lambda + dep) + co;
+        const double f = RIGID ? (al * o.lambda + dep) + rs.rg.C : (al * o.lambda + dep) + co;
+        if (l == 0) rs.f[w] = ml->failed ? __builtin_nan("") : f;
     }
     __syncthreads();
 }
 
 // f_k = cal_cost2(x0, matchId, true) with the spheres of x0 in rs.base.
-template <bool MW, class CV>
+template <bool MW, bool RIGID = false, class CV>
 __device__ __forceinline__ double eval_corr(RefineSm &rs, const DevObs &o, const CV &cv,
                                             const DevHand *__restrict__ H, int32_t *__restrict__ match,
                                             MwLeader *ml, int *flag) {
@@ -1026,7 +1053,7 @@ __device__ __forceinline__ double eval_corr(RefineSm &rs, const DevObs &o, const
     if (young) __builtin_amdgcn_s_setprio(1);
     double al = MW ? 0.0 : search_align<RF_NT, true>(rs.base, cv, H, match, load_pt(cv, t));
     if (young) __builtin_amdgcn_s_setprio(0);
-    double co = (t < 144) ? collide_term(rs.base, t, H) : 0.0;
+    double co = (!RIGID && t < 144) ? collide_term(rs.base, t, H) : 0.0;
     double dep = depth_finish(dg, o, t < HPE_NS);
     block_sum3<RF_NT>(rs.red, al, dep, co);  // also publishes matchId to the block
     if (MW) {
@@ -1034,13 +1061,17 @@ __device__ __forceinline__ double eval_corr(RefineSm &rs, const DevObs &o, const
         al = mw_sum(*ml, 0);
         if (ml->failed) return __builtin_nan("");
     }
+    if (RIGID) return (al * o.lambda + dep) + rs.rg.C;
     return (al * o.lambda + dep) + co;
 }
 
 // Helper workgroup h of a multi-workgroup refine launch: serve jobs until EXIT.
+template <bool RIGID>
 __device__ void mw_helper(const DevMw &mw, int h, const DevObs *__restrict__ og,
                           const DevHand *__restrict__ Hg, int32_t *__restrict__ match_g) {
     __shared__ FkSm nodes[MW_MAX_NODES];
+    __shared__ RigidSm hq;  // RIGID: hand-frame centres, built from the first job's digits
+    bool have_q = false;
     __shared__ DevHand hs;
     __shared__ double red[16][4];
     __shared__ int sh[2];
@@ -1056,11 +1087,11 @@ __device__ void mw_helper(const DevMw &mw, int h, const DevObs *__restrict__ og,
     for (unsigned k = 1;; ++k) {
         if (t == 0) {
             int type = -1, nn = 0;
-            if (mw_wait_geq(&mw.ctr[0], k)) {
+            if (mw_wait_geq(&mw.ctr[0], k, mw.spin)) {
                 type = mw.job->type;
                 nn = mw.job->nnodes;
             } else {
-                atomicExch(mw.err, 1);
+                mw_fail(mw);
             }
             sh[0] = type;
             sh[1] = nn;
@@ -1076,18 +1107,39 @@ __device__ void mw_helper(const DevMw &mw, int h, const DevObs *__restrict__ og,
             return;
         }
         if (type == MW_JOB_CORR) {  // search + alignment over the slice, matchId stored
-            if (t < HPE_DOF) nodes[0].th[t] = mw.job->th[0][t];
+            const double th0 = mw.job->th[0][t < HPE_DOF ? t : 0];
+            if (RIGID && !have_q) {  // the digits are fixed for the whole refine launch
+                if (t < HPE_DOF) nodes[0].th[t] = (t == 0) ? -180.0 : (t < 6) ? 0.0 : th0;
+                __syncthreads();
+                if (w == 0) {
+                    SphXYZ own;
+                    fk_wave(nodes[0], H, &own);
+                    if (l < HPE_NS) {
+                        hq.q[l][0] = own.x;
+                        hq.q[l][1] = own.y * -1;
+                        hq.q[l][2] = own.z * -1;
+                    }
+                }
+                have_q = true;
+                __syncthreads();
+            }
+            if (t < HPE_DOF) nodes[0].th[t] = th0;
             __syncthreads();
-            if (w == 0) fk_wave(nodes[0], H);
+            if (w == 0) {
+                if (RIGID) rigid_wave<RG_ROT>(nodes[0], hq, th0);
+                else fk_wave(nodes[0], H);
+            }
             __syncthreads();
             double al = search_align<RF_NT, true>(nodes[0], cs, H, ms, load_pt(cs, t));
             double z1 = 0.0, z2 = 0.0;
             block_sum3<RF_NT>(red, al, z1, z2);
             if (t == 0) mw.part[h * MW_MAX_NODES] = al;
         } else if (w < nn) {  // one node per wave, frozen matchId of the slice
-            if (l < HPE_DOF) nodes[w].th[l] = mw.job->th[w][l];
+            const double thl = mw.job->th[w][l < HPE_DOF ? l : 0];
+            if (l < HPE_DOF) nodes[w].th[l] = thl;
             wave_sync();
-            fk_wave(nodes[w], H);
+            if (RIGID) rigid_wave<RG_ROT>(nodes[w], hq, thl);  // (Rg q) + u == P + u
+            else fk_wave(nodes[w], H);
             const double al = wave_sum(align_frozen(nodes[w], cs, H, ms, l, 64));
             if (l == 0) mw.part[h * MW_MAX_NODES + w] = al;
         }
@@ -1172,14 +1224,14 @@ __device__ __forceinline__ GoldShape gold_shape(int ctx) {
 // after 30 rejected trials); the accepted node's spheres are copied into rs.base and its
 // cost to *f_acc.  UPD: the search also applies x0 = x0 - tk * g (PSO.cpp:256; gl =
 // component threadIdx.x of g) before its last barrier.  evals grows by the serial count.
-template <bool MW = false, int POL = GOLD_BALANCED, bool UPD = false, class CV>
+template <bool MW = false, int POL = GOLD_BALANCED, bool UPD = false, bool RIGID = false, class CV>
 __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const CV &cv,
                                             const DevHand *__restrict__ H,
                                             const int32_t *__restrict__ match, double fk,
                                             double gp, double pl, double gl, int &evals,
                                             double *f_acc, FkX *Xt = nullptr,
                                             MwLeader *ml = nullptr, int *flag = nullptr,
-                                            const FrozenPts *fp = nullptr) {
+                                            const FrozenPts *fp = nullptr, int rblk = 0) {
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
     StampClock sc;
     sc.start();
@@ -1201,7 +1253,7 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
             thl = rs.x0[l < HPE_DOF ? l : 0] + al2 * pl;
             if (l < HPE_DOF) rs.w[w].th[l] = thl;
         }
-        eval_nodes<MW>(rs, nn, o, cv, H, match, Xt, ml, flag, &thl, fp);
+        eval_nodes<MW, RIGID>(rs, nn, o, cv, H, match, Xt, ml, flag, &thl, fp, rblk);
         if (MW && ml->failed) break;  // the launch is ending early (DevMw::err)
         int node = 0;
         accepted = -1;
@@ -1271,7 +1323,10 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
 // dependencies in the frame loop.
 // MW (clouds > RF_STAGE_MAX): workgroups 1..mw.Q are the helpers of the multi-workgroup
 // form above; the preparation workgroups follow them.
-template <bool STAGED, bool MW = false>
+// RIGID: the hand-frame refine (rigid_wave, hpe_device.hpp): every evaluation of the call
+// places its spheres as Rg q + u from centres q built once from x0's digit angles, the
+// collision a constant of the call; HPE_REFINE_EXACT=1 selects the reference's chain.
+template <bool STAGED, bool MW = false, bool RIGID = false>
 __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, const DevObs *__restrict__ og,
                                                   const DevHand *__restrict__ Hg,
                                                   int32_t *__restrict__ match_g,
@@ -1280,7 +1335,7 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
     extern __shared__ __align__(16) unsigned char dyn[];  // staged cloud + matchId / prep
     const int nhelp = MW ? mw.Q : 0;
     if (MW && blockIdx.x >= 1 && (int)blockIdx.x <= nhelp) {
-        if (do_refine) mw_helper(mw, blockIdx.x - 1, og, Hg, match_g);
+        if (do_refine) mw_helper<RIGID>(mw, blockIdx.x - 1, og, Hg, match_g);
         return;
     }
     if (blockIdx.x >= 1) {
@@ -1320,6 +1375,35 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
     __shared__ int mwflag;
     MwLeader ml{mw, 0u, false};
     __syncthreads();
+    if (RIGID) {
+        // hand-frame centres q (x0's digits, theta0 = -180, theta1..5 = 0: Tgb = I, u = 0)
+        // and the call's constant self-collision penalty
+        if (w == 0) {
+            const double xl = rs.x0[l < HPE_DOF ? l : 0];
+            const double thq = (l == 0) ? -180.0 : (l < 6) ? 0.0 : xl;
+            if (l < HPE_DOF) rs.w[0].th[l] = thq;
+            wave_sync();
+            SphXYZ own;
+            fk_wave<true>(rs.w[0], H, &own, &thq);
+            if (l < HPE_NS) {
+                rs.rg.q[l][0] = own.x;
+                rs.rg.q[l][1] = own.y * -1;
+                rs.rg.q[l][2] = own.z * -1;
+            }
+            CollPair cp[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) cp[k] = collide_load(rs.w[0], k < 2 ? l + 64 * k : ((l < 16) ? l + 128 : l), H);
+            double co = 0.0;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const double v = collide_value(cp[k], sqrt(collide_d2(cp[k])));
+                co += (k < 2 || l < 16) ? v : 0.0;
+            }
+            co = wave_sum(co);
+            if (l == 0) rs.rg.C = co;
+        }
+        __syncthreads();
+    }
     StampClock sc;
     sc.start();
     int evals = 0;
@@ -1333,7 +1417,10 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
         // Block 2 moves only the global position u = x0[3..5]: every FK of the block is
         // the stored rotation terms of x0 plus u (FK_TRANSLATE, bit-identical).
         FkX *Xt = nullptr;
-        if (blk == 1) {
+        if (RIGID && blk == 1) {  // P = Rg q of the block's fixed rotation
+            if (w == 0) rigid_wave<RG_STORE_P>(rs.w[0], rs.rg, rs.x0[l < HPE_DOF ? l : 0], nullptr, rs.rg.P);
+            __syncthreads();
+        } else if (blk == 1) {
             if (w == 0) {
                 if (l < HPE_DOF) rs.w[0].th[l] = rs.x0[l];
                 wave_sync();
@@ -1352,15 +1439,22 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
                 if (t < HPE_DOF) rs.base.th[t] = rs.x0[t];
                 __syncthreads();
                 if (w == 0) {
-                    if (Xt) fk_wave_t<FK_TRANSLATE>(rs.base, H, Xt);
-                    else fk_wave<true>(rs.base, H);
+                    if (RIGID) {
+                        const double thl = rs.x0[l < HPE_DOF ? l : 0];
+                        if (blk) rigid_wave<RG_TRANS>(rs.base, rs.rg, thl);
+                        else rigid_wave<RG_ROT>(rs.base, rs.rg, thl);
+                    } else if (Xt) {
+                        fk_wave_t<FK_TRANSLATE>(rs.base, H, Xt);
+                    } else {
+                        fk_wave<true>(rs.base, H);
+                    }
                 }
                 __syncthreads();
             }
             REF_TS(rs.ts_n, 1);
             double fk;
             if (MW) {
-                fk = eval_corr<MW>(rs, o, cv, H, match, &ml, &mwflag);
+                fk = eval_corr<MW, RIGID>(rs, o, cv, H, match, &ml, &mwflag);
                 REF_TS(rs.ts_n, 2);
                 // cal_grad: x0 +/- e along the 3 block dims, one wave per evaluation
                 if (w < 6) {
@@ -1368,7 +1462,7 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
                     if (l < HPE_DOF)
                         rs.w[w].th[l] = (l == d) ? ((w & 1) ? rs.x0[l] - e : rs.x0[l] + e) : rs.x0[l];
                 }
-                eval_nodes<MW>(rs, 6, o, cv, H, match, Xt, &ml, &mwflag);
+                eval_nodes<MW, RIGID>(rs, 6, o, cv, H, match, Xt, &ml, &mwflag, nullptr, nullptr, blk);
             } else {
                 // f_k = cal_cost2(x0, matchId, true) and cal_grad's six frozen evaluations
                 // (x0 +/- e along the 3 block dims, one wave each) with one barrier between
@@ -1391,7 +1485,7 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
                     al = search_align<RF_NT, true>(rs.base, cv, H, match, load_pt(cv, t));
                 }
                 if (young) __builtin_amdgcn_s_setprio(0);
-                double co = (t < 144) ? collide_term(rs.base, t, H) : 0.0;
+                double co = (!RIGID && t < 144) ? collide_term(rs.base, t, H) : 0.0;
                 const double dep = depth_finish(dgc, o, t < HPE_NS);
                 const double tot = wave_sum((al * o.lambda + dep) + co);  // as block_sum1
                 if (l == 0) rs.red[w][0] = tot;
@@ -1402,16 +1496,20 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
                     const double thl = (l == d) ? ((w & 1) ? xl - e : xl + e) : xl;
                     if (l < HPE_DOF) rs.w[w].th[l] = thl;
                     wave_sync();
-                    hd = frozen_head<true>(rs.w[w], o, H, Xt, &thl);
+                    if (RIGID) hd = blk ? rigid_head<RG_TRANS>(rs.w[w], o, H, rs.rg, thl)
+                                        : rigid_head<RG_ROT>(rs.w[w], o, H, rs.rg, thl);
+                    else hd = frozen_head<true>(rs.w[w], o, H, Xt, &thl);
                 }
                 __syncthreads();  // matchId complete, the corr partial sums in red
                 if (small) load_frozen_pts(fpts, cv, match, l);
                 fk = 0;
 #pragma unroll
                 for (int k = 0; k < RF_NW; ++k) fk += rs.red[k][0];
+                if (RIGID) fk = fk + rs.rg.C;
                 REF_TS(rs.ts_n, 2);
                 if (w < 6) {
-                    const double f = frozen_tail(rs.w[w], o, cv, H, match, hd, small ? &fpts : nullptr);
+                    double f = frozen_tail(rs.w[w], o, cv, H, match, hd, small ? &fpts : nullptr);
+                    if (RIGID) f = f + rs.rg.C;
                     if (l == 0) rs.fg[w] = f;
                 }
                 __syncthreads();
@@ -1442,9 +1540,9 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
             const double gp = (blk == 0) ? (q0 + q2) + q1 : q1 + (q0 + q2);
             // goldstein(x0, grad, matchId, f_k, optfunc, tk, 30)
             // goldstein(x0, grad, matchId, f_k, optfunc, tk, 30), then x0 = x0 - tk*grad
-            const double tk = gold_tree<MW, HPE_GOLD_POLICY, true>(rs, o, cv, H, match, fk, gp, pl, gl,
-                                                                  evals, nullptr, Xt, &ml, &mwflag,
-                                                                  small ? &fpts : nullptr);
+            const double tk = gold_tree<MW, HPE_GOLD_POLICY, true, RIGID>(
+                rs, o, cv, H, match, fk, gp, pl, gl, evals, nullptr, Xt, &ml, &mwflag,
+                small ? &fpts : nullptr, blk);
             sc.lap(22);
             if (tk == 0) cnt += 1;
             // tol = sqrt(sum(grad % grad)): arrayops::accumulate (two accumulators)
@@ -1458,7 +1556,9 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
     }
     if (MW) mw_publish(ml, rs, MW_JOB_EXIT, 0);
     REF_TS(rs.ts_n, 7);
-    if (t < HPE_DOF) x0g[t] = rs.x0[t];
+    // a timed-out multi-workgroup refine has no defined result: the pose becomes NaN, so
+    // this frame's PSO (and its cost) is NaN and never wins an exchange
+    if (t < HPE_DOF) x0g[t] = (MW && ml.failed) ? __builtin_nan("") : rs.x0[t];
     if (t == 0 && evals_out) {
         *evals_out = evals;
         atomicAdd((unsigned long long *)(evals_out + 2), (unsigned long long)evals);  // running total

@@ -127,5 +127,8 @@ struct DevMw {
     unsigned *ctr;   // [0] job sequence; [32 (1 + s)] helper completions of shard s
                      // (helper h -> shard h % MW_DONE_SHARDS); [32 (1 + MW_DONE_SHARDS)] exits
     int *err;        // set when a wait times out (the launch then ends early)
+    int *err_host;   // the same flag in pinned host memory (system-scope store): the next
+                     // tracking call sees it without a synchronisation
     int Q;
+    int spin;        // polls per wait before it counts as timed out (MW_SPIN_MAX; tests)
 };

@@ -79,6 +79,16 @@ class Context:
             pass
 
     # ---- frames
+    @property
+    def refine_exact(self) -> bool:
+        """True: refine_init_pose places spheres by the reference's DH chain on every
+        evaluation; False (default): the hand-frame form (hpe_set_refine_exact)."""
+        return bool(self.lib.hpe_get_refine_exact(self.h))
+
+    @refine_exact.setter
+    def refine_exact(self, exact: bool):
+        self.check(self.lib.hpe_set_refine_exact(self.h, 1 if exact else 0))
+
     def store_frame(self, slot, depth_cm, dt, cloud, scale, dtmax, K):
         depth_cm = np.ascontiguousarray(depth_cm, dtype=np.float64)
         dt = np.ascontiguousarray(dt, dtype=np.float32)

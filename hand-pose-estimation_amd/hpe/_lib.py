@@ -63,6 +63,8 @@ SIGNATURES = {
     "hpe_pso_optimise": (C.c_int, [C.c_void_p, dp, C.c_int, dp, dp, dp, C.c_int]),
     "hpe_pso_trace": (C.c_int, [C.c_void_p, dp, ip, ip, C.c_int]),
     "hpe_refine_init_pose": (C.c_int, [C.c_void_p, dp, ip]),
+    "hpe_set_refine_exact": (C.c_int, [C.c_void_p, C.c_int]),
+    "hpe_get_refine_exact": (C.c_int, [C.c_void_p]),
     "hpe_track_frame": (C.c_int, [C.c_void_p, C.c_int, C.c_int, dp, dp]),
     "hpe_track_frame_dev": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
     "hpe_track_sequence_dev": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int,

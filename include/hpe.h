@@ -165,6 +165,17 @@ int hpe_pso_optimise(hpe_ctx *ctx, const double x0[26], int num_p, double bestp[
 /* PSO::refine_init_pose(x0, optfunc) (PSO.cpp:216-266).  evals_out optional. */
 int hpe_refine_init_pose(hpe_ctx *ctx, double x0[26], int32_t *evals_out);
 
+/* Sphere placement inside refine_init_pose (every refine of this context, including the
+ * tracking loops).  exact = 0 (default): the hand-frame form -- refine moves theta0..5
+ * only (PSO.cpp:225-227), so each evaluation places S = Rg(theta0..2) q + u from centres q
+ * built once per call, and the self-collision penalty is a constant of the call; spheres
+ * within 1e-12 cm and costs within 1e-13 relative of the reference's DH chain
+ * (DESIGN.md §2).  exact = 1: the reference's chain on every evaluation (bit-identical
+ * FK).  The environment variable HPE_REFINE_EXACT=1 sets the default at hpe_create.
+ * Cached tracking graphs are rebuilt on change. */
+int hpe_set_refine_exact(hpe_ctx *ctx, int exact);
+int hpe_get_refine_exact(const hpe_ctx *ctx);
+
 /* One tracked frame of test_full (testmodel.cpp:124-138) on the selected frame:
  * [refine_init_pose] -> pso_evolve -> cost = cal_cost(bestp) -> x0 = bestp.
  * x0_inout: 26 doubles (host).  cost_out optional. */

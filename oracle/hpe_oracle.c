@@ -591,10 +591,31 @@ static void margin_note(double num, double den) {
     const double m = fabs(num) / fabs(den);
     if (!(m >= g_margin)) g_margin = m; /* NaN-safe: a NaN margin counts as a tie */
 }
+/* Per-decision log of the last refine (test instrumentation): decision k's relative margin
+ * (the same measure as margin_note) in g_dec_margin[k], and, for a replay, the decision
+ * whose outcome is inverted (g_flip_at; -1: none).  The sequence tests replay the oracle
+ * with a near-tie flipped and require the GPU's result to equal that replay. */
+static double *g_dec_margin = NULL;
+static int g_dec_cap = 0, g_dec_n = 0;
+static const int *g_flips = NULL;
+static int g_nflips = 0;
+static int decide(int outcome, double num, double den) {
+    if (!g_margin_on) return outcome; /* pso_optimise's searches (OpenMP): no log */
+    margin_note(num, den);
+    const int k = g_dec_n++;
+    if (g_dec_margin && k < g_dec_cap) g_dec_margin[k] = fabs(num) / fabs(den);
+    for (int i = 0; i < g_nflips; ++i)
+        if (g_flips[i] == k) return !outcome;
+    return outcome;
+}
 
 /* goldstein, PSO.cpp:438-480 */
+struct rigid_ctx;
+static double rigid_cost2(const struct rigid_ctx *r, const ora_hand *h, const ora_obs *o,
+                          const double th[26], int32_t *match, int compute_corr);
 static double goldstein(const ora_hand *h, const ora_obs *o, const double *theta,
-                        const double *g, int32_t *match, double fk, int maxiter, int *evals) {
+                        const double *g, int32_t *match, double fk, int maxiter, int *evals,
+                        const struct rigid_ctx *rg) {
     double a = 0, b = 1e100, alpha = 0.5;
     uint64_t path = 0;
     const double t = 2, c = 0.25;
@@ -602,15 +623,14 @@ static double goldstein(const ora_hand *h, const ora_obs *o, const double *theta
     for (int d = 0; d < 26; ++d) p[d] = -1 * g[d];
     for (int it = 0; it < maxiter; ++it) {
         for (int d = 0; d < 26; ++d) th1[d] = theta[d] + alpha * p[d];
-        const double f1 = ora_cal_cost2(h, o, th1, match, 0, NULL);
+        const double f1 = rg ? rigid_cost2(rg, h, o, th1, match, 0)
+                             : ora_cal_cost2(h, o, th1, match, 0, NULL);
         ++*evals;
         const double gp = dot2(g, p, 26);
         const double armijo = fk + c * alpha * gp;
         const double gold = fk + (1 - c) * alpha * gp;
-        margin_note(f1 - armijo, fk);
-        if (f1 <= armijo) {
-            margin_note(f1 - gold, fk);
-            if (f1 >= gold) {
+        if (decide(f1 <= armijo, f1 - armijo, fk)) {
+            if (decide(f1 >= gold, f1 - gold, fk)) {
                 gold_log(path, it + 1, 1);
                 return alpha;
             }
@@ -627,20 +647,104 @@ static double goldstein(const ora_hand *h, const ora_obs *o, const double *theta
     return 0;
 }
 
-/* refine_init_pose + cal_grad, PSO.cpp:183-266.  Returns number of cost evals. */
-int ora_refine_init_pose(const ora_hand *h, const ora_obs *o, double x0[26]) {
+/* ---- the GPU's hand-frame refine (TEST INFRASTRUCTURE: not the reference's operation
+ * order).  refine_init_pose moves theta0..5 only (PSO.cpp:225-227), so the GPU's default
+ * refine (k_refine<..., RIGID>, hpe_device.hpp rigid_wave) places every sphere of the call
+ * as negate_yz(Rg(theta0..2) q_k + u) from hand-frame centres q_k (this FK at theta0 = -180,
+ * theta1..5 = 0, y and z un-negated) and adds the call's constant self-collision penalty.
+ * This mirror repeats the GPU's operations, so the GPU's rigid refine is compared with it
+ * exactly as the chain refine is compared with ora_refine_init_pose; the tests bound the
+ * mirror's distance from the reference order separately (tests/test_rigid.py). */
+struct rigid_ctx {
+    double q[ORA_NS * 3];
+    double C;
+};
+
+static void rigid_init(struct rigid_ctx *r, const ora_hand *h, const double x0[26]) {
+    double th[26];
+    memcpy(th, x0, sizeof(th));
+    th[0] = -180;
+    for (int d = 1; d < 6; ++d) th[d] = 0;
+    ora_build_hand_model(h, th, r->q, NULL);
+    for (int i = 0; i < ORA_NS; ++i) {
+        r->q[3 * i + 1] *= -1;
+        r->q[3 * i + 2] *= -1;
+    }
+    r->C = ora_collision(h, r->q);
+}
+
+/* rows of Rg = Rz(theta0 + 180) Ry(theta1) Rx(theta2) as hpe_device.hpp rigid_row */
+static void rigid_rows(const double th[3], double G[9]) {
+    const double az = deg2rad(th[0] + 180), ay = deg2rad(th[1]), ax = deg2rad(th[2]);
+    const double sz = sin(az), cz = cos(az), sy = sin(ay), cy = cos(ay);
+    const double sx = sin(ax), cx = cos(ax);
+    for (int r = 0; r < 3; ++r) {
+        double z0, z1, z2;
+        if (r == 0) { z0 = cz; z1 = -sz; z2 = 0; }
+        else if (r == 1) { z0 = sz; z1 = cz; z2 = 0; }
+        else { z0 = 0; z1 = 0; z2 = 1; }
+        const double q0 = z0 * cy + z2 * (-sy), q1 = z1, q2 = z0 * sy + z2 * cy;
+        G[3 * r] = q0;
+        G[3 * r + 1] = q1 * cx + q2 * sx;
+        G[3 * r + 2] = q1 * (-sx) + q2 * cx;
+    }
+}
+
+void ora_rigid_spheres(const ora_hand *h, const double x0[26], const double th[26],
+                       double S[144]) {
+    struct rigid_ctx r;
+    rigid_init(&r, h, x0);
+    double G[9];
+    rigid_rows(th, G);
+    for (int k = 0; k < ORA_NS; ++k)
+        for (int c = 0; c < 3; ++c) {
+            const double *q = r.q + 3 * k;
+            const double v = ((G[3 * c] * q[0] + G[3 * c + 1] * q[1]) + G[3 * c + 2] * q[2]) + th[3 + c];
+            S[3 * k + c] = (c == 0) ? v : v * -1;
+        }
+}
+
+static double rigid_cost2(const struct rigid_ctx *r, const ora_hand *h, const ora_obs *o,
+                          const double th[26], int32_t *match, int compute_corr) {
+    double G[9], S[144];
+    rigid_rows(th, G);
+    for (int k = 0; k < ORA_NS; ++k)
+        for (int c = 0; c < 3; ++c) {
+            const double *q = r->q + 3 * k;
+            const double v = ((G[3 * c] * q[0] + G[3 * c + 1] * q[1]) + G[3 * c + 2] * q[2]) + th[3 + c];
+            S[3 * k + c] = (c == 0) ? v : v * -1;
+        }
+    if (compute_corr) ora_correspondences(o, S, match);
+    const double a = ora_align(h, o, S, match);
+    const double d = ora_depth_penalty(h, o, S);
+    return (a + d) + r->C;
+}
+
+/* refine_init_pose + cal_grad, PSO.cpp:183-266.  Returns number of cost evals.
+ * rigid != 0: the GPU's hand-frame mirror above (test infrastructure). */
+int ora_refine_ex(const ora_hand *h, const ora_obs *o, double x0[26], int rigid,
+                  const int *flips, int nflips, double *margins, int cap, int *ndec) {
     const int start_idx[2] = {0, 3}, end_idx[2] = {2, 5};
     int32_t *match = (int32_t *)malloc(sizeof(int32_t) * (o->n > 0 ? o->n : 1));
     int evals = 0;
+    struct rigid_ctx rg;
+    if (rigid) rigid_init(&rg, h, x0);
+    const struct rigid_ctx *rp = rigid ? &rg : NULL;
     g_margin_on = 1;
     g_margin = INFINITY;
+    g_dec_margin = margins;
+    g_dec_cap = margins ? cap : 0;
+    g_dec_n = 0;
+    g_flips = flips;
+    g_nflips = flips ? nflips : 0;
     for (int blk = 0; blk < 2; ++blk) {
         const double eps = 1e-6;
         double tol = 1;
         int cnt = 0, iter = 0;
         const int maxiter = 15;
-        while (tol > eps && iter < maxiter && cnt < 1) {
-            const double fk = ora_cal_cost2(h, o, x0, match, 1, NULL);
+        while (iter < maxiter && cnt < 1 && (iter == 0 || decide(tol > eps, tol - eps, eps))) {
+            const double fk = rp ? rigid_cost2(rp, h, o, x0, match, 1)
+                                 : ora_cal_cost2(h, o, x0, match, 1, NULL);
             evals++;
             double grad[26];
             for (int i = 0; i < 26; ++i) {
@@ -652,25 +756,34 @@ int ora_refine_init_pose(const ora_hand *h, const ora_obs *o, double x0[26]) {
                     memcpy(xmh, x0, sizeof(xmh));
                     xph[i] += e;
                     xmh[i] -= e;
-                    const double fp = ora_cal_cost2(h, o, xph, match, 0, NULL);
-                    const double fm = ora_cal_cost2(h, o, xmh, match, 0, NULL);
+                    const double fp = rp ? rigid_cost2(rp, h, o, xph, match, 0)
+                                         : ora_cal_cost2(h, o, xph, match, 0, NULL);
+                    const double fm = rp ? rigid_cost2(rp, h, o, xmh, match, 0)
+                                         : ora_cal_cost2(h, o, xmh, match, 0, NULL);
                     evals += 2;
                     grad[i] = (fp - fm) / (2 * e);
                 }
             }
-            const double tk = goldstein(h, o, x0, grad, match, fk, 30, &evals);
+            const double tk = goldstein(h, o, x0, grad, match, fk, 30, &evals, rp);
             if (tk == 0) cnt += 1;
             for (int d = 0; d < 26; ++d) x0[d] = x0[d] - tk * grad[d];
             double g2[26];
             for (int d = 0; d < 26; ++d) g2[d] = grad[d] * grad[d];
             tol = sqrt(accumulate2(g2, 26));
-            margin_note(tol - eps, eps);
             iter += 1;
         }
     }
     g_margin_on = 0;
+    g_dec_margin = NULL;
+    g_flips = NULL;
+    g_nflips = 0;
+    if (ndec) *ndec = g_dec_n;
     free(match);
     return evals;
+}
+
+int ora_refine_init_pose(const ora_hand *h, const ora_obs *o, double x0[26]) {
+    return ora_refine_ex(h, o, x0, 0, NULL, 0, NULL, 0, NULL);
 }
 
 /* pso_optimise, PSO.cpp:539-712: each generation every particle first runs graditer = 10
@@ -733,7 +846,7 @@ int ora_pso_optimise(const ora_hand *h, const ora_obs *o, const double x0[26], i
                 for (int d = 0; d < D; ++d) grad[d] = 0;
                 grad[sel] = (fp - fm) / (2 * e);
                 int ev = 0;
-                const double tk = goldstein(h, o, th, grad, match, fk, 30, &ev);
+                const double tk = goldstein(h, o, th, grad, match, fk, 30, &ev, NULL);
                 for (int d = 0; d < D; ++d) th[d] = th[d] - tk * grad[d];
                 const double f2 = ora_cal_cost2(h, o, th, match, corr, NULL);
                 if (f2 < pc[i]) {

@@ -88,6 +88,15 @@ int ora_pso_evolve(const ora_hand *h, const ora_obs *o, const double x0[26], int
                    double *bestcost, ora_pso_trace *trace, int nthreads);
 
 int ora_refine_init_pose(const ora_hand *h, const ora_obs *o, double x0[26]);
+/* The same with test instrumentation: rigid != 0 runs the mirror of the GPU's hand-frame
+ * refine (NOT the reference's operation order; hpe_oracle.c); margins[0..cap) receives
+ * every decision's relative margin, *ndec their number; the decisions numbered
+ * flips[0..nflips) have their outcome inverted (near-tie replay). */
+int ora_refine_ex(const ora_hand *h, const ora_obs *o, double x0[26], int rigid,
+                  const int *flips, int nflips, double *margins, int cap, int *ndec);
+/* spheres of theta by the hand-frame mirror, centres q built from x0's digits */
+void ora_rigid_spheres(const ora_hand *h, const double x0[26], const double th[26],
+                       double S[144]);
 /* test instrumentation: smallest relative decision margin of the last refine */
 double ora_refine_last_margin(void);
 /* diagnostic: log every Goldstein search's decisions into buf (see hpe_oracle.c) */

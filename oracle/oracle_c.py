@@ -88,6 +88,12 @@ class Oracle:
         L.ora_refine_init_pose.argtypes = [C.POINTER(OraHand), C.POINTER(OraObs), dp]
         L.ora_refine_init_pose.restype = C.c_int
         L.ora_refine_last_margin.restype = C.c_double
+        L.ora_refine_ex.argtypes = [C.POINTER(OraHand), C.POINTER(OraObs), dp, C.c_int,
+                                    C.POINTER(C.c_int), C.c_int, dp, C.c_int,
+                                    C.POINTER(C.c_int)]
+        L.ora_refine_ex.restype = C.c_int
+        L.ora_rigid_spheres.argtypes = [C.POINTER(OraHand), dp, dp, dp]
+        L.ora_rigid_spheres.restype = None
         L.ora_gnd_truth_err.argtypes = [dp, dp, C.c_int, C.c_int]
         L.ora_gnd_truth_err.restype = C.c_double
         L.ora_dist_transform.argtypes = [dp, fp]
@@ -189,10 +195,38 @@ class Oracle:
                                   _p(tg, C.c_double), nthreads)
         return bp, bc.value, tg[:max(maxiter - 1, 0)]
 
-    def refine(self, h, obs, x0):
+    def refine(self, h, obs, x0, rigid=False):
+        """refine_init_pose (PSO.cpp:183-266); rigid=True: the mirror of the GPU's default
+        hand-frame refine (test infrastructure, not the reference's operation order)."""
         x = np.array(x0, dtype=np.float64)
-        ev = self.lib.ora_refine_init_pose(C.byref(h), C.byref(obs.s), _p(x, C.c_double))
+        if rigid:
+            ev = self.lib.ora_refine_ex(C.byref(h), C.byref(obs.s), _p(x, C.c_double), 1, None,
+                                        0, None, 0, None)
+        else:
+            ev = self.lib.ora_refine_init_pose(C.byref(h), C.byref(obs.s), _p(x, C.c_double))
         return x, ev
+
+    def refine_log(self, h, obs, x0, rigid=False, flips=(), cap=4096):
+        """refine with the decision log: (x, evals, margins) where margins[k] is decision
+        k's relative margin; the decisions numbered in flips are inverted (near-tie
+        replay)."""
+        x = np.array(x0, dtype=np.float64)
+        m = np.zeros(cap)
+        nd = C.c_int(0)
+        fl = np.ascontiguousarray(list(flips), dtype=np.int32)
+        ev = self.lib.ora_refine_ex(C.byref(h), C.byref(obs.s), _p(x, C.c_double),
+                                    1 if rigid else 0, _p(fl, C.c_int) if len(fl) else None,
+                                    len(fl), _p(m, C.c_double), cap, C.byref(nd))
+        return x, ev, m[:min(nd.value, cap)].copy()
+
+    def rigid_spheres(self, h, x0, theta):
+        """Spheres of theta by the hand-frame mirror (centres from x0's digits), 48 x 3."""
+        a = np.ascontiguousarray(x0, dtype=np.float64)
+        t = np.ascontiguousarray(theta, dtype=np.float64)
+        S = np.zeros(144)
+        self.lib.ora_rigid_spheres(C.byref(h), _p(a, C.c_double), _p(t, C.c_double),
+                                   _p(S, C.c_double))
+        return S.reshape(48, 3)
 
     def refine_last_margin(self):
         """The smallest relative decision margin of the last refine() (test

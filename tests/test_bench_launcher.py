@@ -29,6 +29,12 @@ def test_self_launch_two_ranks_stub():
     # frame 3: rank 0 has cost 10 + 3 % 2 = 11, rank 1 10 + 10 % 2 = 10 -> rank 1 wins
     assert r["winner_rank"] == 1 and r["winner_cost"] == 10.0
     assert r["value"] > 0
+    # the multi-rank self-verification (bench.py rank_report)
+    rk = r["ranks"]
+    assert rk["world_size_pg"] == 2 and rk["backend"] == "gloo"
+    assert rk["devices_distinct"] and len(rk["devices"]) == 2
+    assert rk["final_state_identical"]
+    assert 0 < rk["ms_per_step_min"] <= rk["ms_per_step_max"]
 
 
 def test_single_rank_stub():

@@ -15,6 +15,7 @@ import numpy as np
 import pytest
 
 import hand_data
+from hand_data import REFINE_RIGID
 import oracle_np
 
 pytestmark = pytest.mark.gpu
@@ -34,6 +35,14 @@ def test_bench_two_ranks_same_device_gloo(tmp_path, oracle, ora_hand):
     assert len(lines) == 1, out.stdout
     r = json.loads(lines[0])
     assert r["n_gpus"] == 2 and r["config"]["particles"] == 1024 and r["value"] > 0
+    # the multi-rank self-verification the 8-GPU run will carry (bench.py rank_report)
+    rk = r["ranks"]
+    assert rk["world_size_pg"] == 2 and rk["backend"] == "gloo" and rk["same_device_mode"]
+    assert len(rk["devices"]) == 2 and not rk["devices_distinct"]  # both on cuda:0
+    assert all(d["pci"] == rk["devices"][0]["pci"] for d in rk["devices"])
+    assert rk["final_state_identical"]
+    assert 0 < rk["ms_per_step_min"] <= rk["ms_per_step_max"]
+    assert rk["exchange_us"]["frames"] == 3 and rk["exchange_us"]["mean"] > 0
     st = [np.load(dump / f"states_rank{k}.npy") for k in range(2)]
     assert st[0].shape == (4, 27)
     np.testing.assert_array_equal(st[0], st[1])  # every rank adopts the same winner
@@ -42,7 +51,7 @@ def test_bench_two_ranks_same_device_gloo(tmp_path, oracle, ora_hand):
     ub, lb, sd = oracle_np.reference_bounds()
     res = []
     for rank in range(2):
-        xr, _ = oracle.refine(ora_hand, obs, x0)
+        xr, _ = oracle.refine(ora_hand, obs, x0, rigid=REFINE_RIGID)
         xr, _, _ = oracle.pso_evolve(ora_hand, obs, xr, 1024, 31, lb, ub, sd, seed=1000 + rank)
         res.append((oracle.cal_cost(ora_hand, obs, xr), rank, xr))
     assert res[0][0] != res[1][0]

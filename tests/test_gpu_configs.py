@@ -20,6 +20,7 @@ import numpy as np
 import pytest
 
 import hand_data
+from hand_data import REFINE_RIGID
 import oracle_np
 
 pytestmark = pytest.mark.gpu
@@ -32,6 +33,14 @@ SEQ_POSE_TOL, SEQ_COST_RTOL = 2e-6, 1e-7  # long sequences (test_config3)
 # smallest margin is ~1e-5; the fp64 sums' order alone moves a cost by ~1e-16 relative;
 # measured: the 9 mismatched frames of the 400-frame sequence at 1.6e-16 .. 2.4e-15)
 TIE_MARGIN = 1e-13
+
+
+def _tie_replay(oracle, ora_hand, obs, x0, gpu_evals):
+    """A refine whose evaluation count differs from the oracle's must be the oracle's own
+    run with near-tie decisions (margin < TIE_MARGIN) inverted: hand_data.tie_replay
+    replays one, then two, flipped ties and returns the flips whose replay takes exactly
+    the GPU's evaluation count (None: no near-tie explains it)."""
+    return hand_data.tie_replay(oracle, ora_hand, obs, x0, gpu_evals, REFINE_RIGID, TIE_MARGIN)
 
 
 @pytest.fixture(scope="module")
@@ -92,7 +101,7 @@ def test_config2_single_frame_256x30(oracle, ora_hand, gh, downsample):
     # the same frame as a tracked frame: refine, pso_evolve, cal_cost(bestp)
     x = x0.copy()
     c = pso.track_frame(cf, x, P, refine=True)
-    xr, _ = oracle.refine(ora_hand, obs, x0)
+    xr, _ = oracle.refine(ora_hand, obs, x0, rigid=REFINE_RIGID)
     xr, _, _ = oracle.pso_evolve(ora_hand, obs, xr, P, maxiter, lb, ub, sd, seed=1000)
     cr = oracle.cal_cost(ora_hand, obs, xr)
     np.testing.assert_allclose(x, xr, rtol=0, atol=POSE_TOL)
@@ -213,22 +222,21 @@ def test_config3_full_cloud_20_frames_pipelined(oracle, ora_hand, gh):
         obs = oracle.preprocess(raw[f], downsample=False)
         assert obs.n > 2048
         x0 = poses[0] if f == 0 else gx[f - 1]
-        xr, er = oracle.refine(ora_hand, obs, x0)
+        xr, er = oracle.refine(ora_hand, obs, x0, rigid=REFINE_RIGID)
         margin.append(oracle.refine_last_margin())
         xr, _, _ = oracle.pso_evolve(ora_hand, obs, xr, P, maxiter, lb, ub, sd, seed=1000)
         cr = oracle.cal_cost(ora_hand, obs, xr)
         dpose.append(np.abs(gx[f] - xr).max())
         assert _cost_eq(gc[f], cr, SEQ_COST_RTOL), (f, gc[f], cr)
         if gev[f] != er:
-            ev_mismatch.append(f)
+            ev_mismatch.append((f, _tie_replay(oracle, ora_hand, obs, x0, gev[f])))
     dpose, margin = np.array(dpose), np.array(margin)
     print(f"{n} full-cloud frames: max |dpose| {dpose.max():.3g} (frame {int(dpose.argmax())}), "
-          f"refine eval-count mismatches {len(ev_mismatch)} {ev_mismatch}, their decision "
-          f"margins {margin[ev_mismatch]}; frames with a margin < {TIE_MARGIN:g}: "
-          f"{int((margin < TIE_MARGIN).sum())}")
+          f"refine eval-count mismatches (frame, flipped tie's margin) {ev_mismatch}; frames "
+          f"with a margin < {TIE_MARGIN:g}: {int((margin < TIE_MARGIN).sum())}")
     assert dpose.max() <= SEQ_POSE_TOL, f"frame {int(dpose.argmax())}: pose {dpose.max()}"
     assert len(ev_mismatch) <= max(1, n // 20)
-    assert np.all(margin[ev_mismatch] < TIE_MARGIN), "an eval-count mismatch without a near-tie"
+    assert all(m is not None for _, m in ev_mismatch), "an eval-count mismatch no near-tie explains"
 
 
 def test_config3_sequence_400_frames_pipelined(oracle, ora_hand, gh):
@@ -245,9 +253,10 @@ def test_config3_sequence_400_frames_pipelined(oracle, ora_hand, gh):
     Goldstein comparisons (PSO.cpp:459-474) sit at that rounding floor once alpha * g'p is
     ~1e-13: on ~2 % of frames a decision flips, the refine takes a few evaluations more or
     fewer and the pose moves by up to ~1e-6 (measured on this sequence: 9 of 400 frames,
-    max 9.6e-7; free-running drift max 3.5e-7).  Each such frame must have
-    flipped a near-tie: the oracle's refine from the same x0 took a decision with a
-    relative margin below TIE_MARGIN.  Single calls keep the exact eval count
+    max 9.6e-7; free-running drift max 3.5e-7).  Each such frame must
+    be the oracle's refine from the same x0 with one near-tie decision (relative margin
+    below TIE_MARGIN) inverted: replaying the oracle with that decision flipped takes
+    exactly the GPU's evaluation count (_tie_replay).  Single calls keep the exact eval count
     (test_gpu_parity.py)."""
     n, P, maxiter = 400, 256, 31
     poses = hand_data.trajectory(n, seed=7, revert=0.02)  # stays in view
@@ -259,7 +268,7 @@ def test_config3_sequence_400_frames_pipelined(oracle, ora_hand, gh):
     for f in range(n):
         obs = oracle.preprocess(raw[f])
         x0 = poses[0] if f == 0 else gx[f - 1]
-        xr, er = oracle.refine(ora_hand, obs, x0)
+        xr, er = oracle.refine(ora_hand, obs, x0, rigid=REFINE_RIGID)
         margin.append(oracle.refine_last_margin())
         xr, _, _ = oracle.pso_evolve(ora_hand, obs, xr, P, maxiter, lb, ub, sd, seed=1000)
         cr = oracle.cal_cost(ora_hand, obs, xr)
@@ -267,8 +276,8 @@ def test_config3_sequence_400_frames_pipelined(oracle, ora_hand, gh):
         dcost.append(0.0 if _cost_eq(gc[f], cr, SEQ_COST_RTOL) and np.isnan(cr)
                      else abs(gc[f] - cr) / abs(cr))
         if gev[f] != er:
-            ev_mismatch.append(f)
-        free, _ = oracle.refine(ora_hand, obs, free)
+            ev_mismatch.append((f, _tie_replay(oracle, ora_hand, obs, x0, gev[f])))
+        free, _ = oracle.refine(ora_hand, obs, free, rigid=REFINE_RIGID)
         free, _, _ = oracle.pso_evolve(ora_hand, obs, free, P, maxiter, lb, ub, sd, seed=1000)
         drift.append(np.abs(free - gx[f]).max())
     dpose, dcost, drift, margin = np.array(dpose), np.array(dcost), np.array(drift), np.array(margin)
@@ -276,13 +285,13 @@ def test_config3_sequence_400_frames_pipelined(oracle, ora_hand, gh):
     print(f"400 frames: per-frame max |dpose| {dpose.max():.3g} (frame {int(dpose.argmax())}), "
           f"max dcost {np.nanmax(dcost):.3g}, refine eval-count mismatches {len(ev_mismatch)} "
           f"{ev_mismatch[:10]}; free-running oracle: max drift {drift.max():.3g}, first frame "
-          f"beyond {POSE_TOL:g}: {first(drift, POSE_TOL)}; mismatched frames' decision margins "
-          f"{margin[ev_mismatch]}; frames with a margin < {TIE_MARGIN:g}: "
+          f"beyond {POSE_TOL:g}: {first(drift, POSE_TOL)}; mismatched frames (frame, flipped "
+          f"tie's margin) {ev_mismatch}; frames with a margin < {TIE_MARGIN:g}: "
           f"{int((margin < TIE_MARGIN).sum())}, median margin {np.median(margin):.3g}")
     assert dpose.max() <= SEQ_POSE_TOL, f"frame {int(dpose.argmax())}: pose {dpose.max()}"
     assert np.all(dcost <= SEQ_COST_RTOL), f"frame {int(np.nanargmax(dcost))}: cost {dcost.max()}"
     assert len(ev_mismatch) <= n // 20
-    assert np.all(margin[ev_mismatch] < TIE_MARGIN), "an eval-count mismatch without a near-tie"
+    assert all(m is not None for _, m in ev_mismatch), "an eval-count mismatch no near-tie explains"
     assert drift.max() <= 10 * SEQ_POSE_TOL, f"free-running divergence from frame {first(drift, 10 * SEQ_POSE_TOL)}"
 
 
@@ -298,7 +307,7 @@ def test_config1_hpe_track_32x10(tmp_path, oracle, ora_hand, np_hand):
     ref_c, ref_x = [], []
     for f in range(n):
         obs = oracle.preprocess(depth[f])
-        x, _ = oracle.refine(ora_hand, obs, x)
+        x, _ = oracle.refine(ora_hand, obs, x, rigid=REFINE_RIGID)
         x, _, _ = oracle.pso_evolve(ora_hand, obs, x, P, maxiter, lb, ub, sd)
         ref_c.append(oracle.cal_cost(ora_hand, obs, x))
         ref_x.append(x.copy())

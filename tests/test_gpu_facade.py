@@ -14,6 +14,7 @@ import numpy as np
 import pytest
 
 import hand_data
+from hand_data import REFINE_RIGID
 import oracle_np
 
 pytestmark = pytest.mark.gpu
@@ -59,7 +60,7 @@ def test_cpp_driver_matches_oracle(tmp_path, oracle, ora_hand, np_hand):
     ref_c, ref_x = [], []
     for f in range(n):
         obs = oracle.preprocess(depth[f])
-        x, _ = oracle.refine(ora_hand, obs, x)
+        x, _ = oracle.refine(ora_hand, obs, x, rigid=REFINE_RIGID)
         x, _, _ = oracle.pso_evolve(ora_hand, obs, x, P, maxiter, lb, ub, sd)
         ref_c.append(oracle.cal_cost(ora_hand, obs, x))
         ref_x.append(x.copy())

@@ -14,6 +14,7 @@ import numpy as np
 import pytest
 
 import hand_data
+from hand_data import REFINE_RIGID
 import oracle_np
 
 pytestmark = pytest.mark.gpu
@@ -43,6 +44,22 @@ def _obs_pair(oracle, gpu_hand, depth_mm, downsample=True):
     om.to_cm, om.downsample, om.focal_len = True, downsample, 241.42
     om.set_depth_mm(depth_mm)
     return obs, om
+
+
+class _refine_form:
+    """Run a test body with the context's refine in one form (hpe_set_refine_exact), the
+    oracle mode to compare with as the value: rigid (the hand-frame mirror) unless exact."""
+
+    def __init__(self, ctx, exact):
+        self.ctx, self.exact = ctx, exact
+
+    def __enter__(self):
+        self.prev = self.ctx.refine_exact
+        self.ctx.refine_exact = self.exact
+        return not self.exact
+
+    def __exit__(self, *exc):
+        self.ctx.refine_exact = self.prev
 
 
 def _match_equiv(obs, S, m_gpu, m_ref):
@@ -214,23 +231,32 @@ def test_pso_optimise(oracle, ora_hand, gpu_hand, np_hand, P, maxiter, downsampl
     assert tr[-1] <= tr[0]
 
 
-def test_refine_init_pose(oracle, ora_hand, gpu_hand, np_hand):
+@pytest.mark.parametrize("exact", [False, True])
+def test_refine_init_pose(oracle, ora_hand, gpu_hand, np_hand, exact):
+    """Both refine forms: the hand-frame one (default) against the oracle's mirror of it,
+    the reference's chain (HPE_REFINE_EXACT) against the restatement; the exact evaluation
+    count either way."""
     import hpe
     truth = hand_data.trajectory(2, seed=4)[1]
     d = oracle_np.render_depth_mm(np_hand, truth)
     obs, om = _obs_pair(oracle, gpu_hand, d)
     cf = hpe.costfunc(gpu_hand, om)
     x0 = oracle_np.X0.copy()
-    x_ref, ev_ref = oracle.refine(ora_hand, obs, x0)
-    pso = hpe.PSO()
-    x = x0.copy()
-    pso.refine_init_pose(x, cf)
+    with _refine_form(gpu_hand.ctx, exact) as rigid:
+        x_ref, ev_ref = oracle.refine(ora_hand, obs, x0, rigid=rigid)
+        pso = hpe.PSO()
+        x = x0.copy()
+        pso.refine_init_pose(x, cf)
     assert pso.last_refine_evals == ev_ref
     np.testing.assert_allclose(x, x_ref, rtol=0, atol=1e-6)
+    # and the hand-frame form is within the tracking tolerance of the reference's order
+    x_chain, _ = oracle.refine(ora_hand, obs, x0, rigid=False)
+    np.testing.assert_allclose(x, x_chain, rtol=0, atol=1e-6)
 
 
+@pytest.mark.parametrize("exact", [False, True])
 @pytest.mark.parametrize("npts", [256, 257, 1500])
-def test_refine_staged_cloud_sizes(oracle, ora_hand, gpu_hand, np_hand, npts):
+def test_refine_staged_cloud_sizes(oracle, ora_hand, gpu_hand, np_hand, npts, exact):
     """refine_init_pose on clouds staged in LDS at the sizes around its two paths: N <= 256
     keeps each lane's matchIds in registers and spreads the correspondence items by SIMD
     load; 256 < N <= 2048 runs the plain strided search and LDS alignment.  The frame keeps
@@ -246,16 +272,18 @@ def test_refine_staged_cloud_sizes(oracle, ora_hand, gpu_hand, np_hand, npts):
     assert obs.n == npts
     cf = hpe.costfunc(gpu_hand, om)
     x0 = oracle_np.X0.copy()
-    x_ref, ev_ref = oracle.refine(ora_hand, obs, x0)
-    pso = hpe.PSO()
-    x = x0.copy()
-    pso.refine_init_pose(x, cf)
+    with _refine_form(gpu_hand.ctx, exact) as rigid:
+        x_ref, ev_ref = oracle.refine(ora_hand, obs, x0, rigid=rigid)
+        pso = hpe.PSO()
+        x = x0.copy()
+        pso.refine_init_pose(x, cf)
     assert pso.last_refine_evals == ev_ref
     np.testing.assert_allclose(x, x_ref, rtol=0, atol=1e-6)
 
 
+@pytest.mark.parametrize("exact", [False, True])
 @pytest.mark.parametrize("mw", ["1", "0"])
-def test_refine_full_cloud(oracle, ora_hand, np_hand, mw, monkeypatch):
+def test_refine_full_cloud(oracle, ora_hand, np_hand, mw, exact, monkeypatch):
     """refine_init_pose on a full-resolution cloud (> 2048 points): the multi-workgroup
     form (mw=1: 64 helper workgroups own cloud slices, partial sums folded in a fixed
     order) and the single-workgroup form (HPE_REFINE_MW=0) both match the oracle, with
@@ -269,7 +297,8 @@ def test_refine_full_cloud(oracle, ora_hand, np_hand, mw, monkeypatch):
     assert obs.n > 2048
     cf = hpe.costfunc(gh, om)
     x0 = oracle_np.X0.copy()
-    x_ref, ev_ref = oracle.refine(ora_hand, obs, x0)
+    gh.ctx.refine_exact = exact
+    x_ref, ev_ref = oracle.refine(ora_hand, obs, x0, rigid=not exact)
     pso = hpe.PSO()
     x = x0.copy()
     pso.refine_init_pose(x, cf)
@@ -295,7 +324,7 @@ def test_track_sequence(oracle, ora_hand, gpu_hand, np_hand):
         om.set_depth_mm(d)
         obs = oracle.preprocess(d)
         c = pso.track_frame(cf, x_gpu, 32, refine=True)
-        x_ref, _ = oracle.refine(ora_hand, obs, x_ref)
+        x_ref, _ = oracle.refine(ora_hand, obs, x_ref, rigid=REFINE_RIGID)
         x_ref, _, _ = oracle.pso_evolve(ora_hand, obs, x_ref, 32, 6, lb, ub, sd)
         cr = oracle.cal_cost(ora_hand, obs, x_ref)
         np.testing.assert_allclose(x_gpu, x_ref, rtol=0, atol=1e-6)
@@ -339,7 +368,7 @@ def test_edge_large_cloud(oracle, ora_hand, gpu_hand, np_hand):
     th = np.vstack([truth, truth + 2, oracle_np.X0])
     np.testing.assert_allclose(cf.cal_cost_batch(th), oracle.eval_costs(ora_hand, obs, th),
                                rtol=RTOL)
-    x_ref, ev_ref = oracle.refine(ora_hand, obs, truth.copy())
+    x_ref, ev_ref = oracle.refine(ora_hand, obs, truth.copy(), rigid=REFINE_RIGID)
     pso = hpe.PSO()
     x = truth.copy()
     pso.refine_init_pose(x, cf)
@@ -368,7 +397,7 @@ def test_edge_empty_frame_optimisers(oracle, ora_hand, gpu_hand):
     assert pso.last_gbest_cost == rc
     x = x0.copy()
     pso.refine_init_pose(x, cf)
-    xr, evr = oracle.refine(ora_hand, obs, x0)
+    xr, evr = oracle.refine(ora_hand, obs, x0, rigid=REFINE_RIGID)
     np.testing.assert_array_equal(x, xr)
     assert pso.last_refine_evals == evr
     pso.pso_optimise(cf, x0, 4, bp)

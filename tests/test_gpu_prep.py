@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 import hand_data
+from hand_data import REFINE_RIGID
 import oracle_np
 
 pytestmark = pytest.mark.gpu
@@ -83,7 +84,7 @@ def test_prepared_frames_track_like_oracle(gh, oracle, ora_hand, np_hand):
         gh.ctx.check(gh.ctx.lib.hpe_track_frame(gh.ctx.h, 32, 1, ptr(x_gpu, C.c_double),
                                                 C.byref(cost)))
         obs = oracle.preprocess(depth[f])
-        x_ref, _ = oracle.refine(ora_hand, obs, x_ref)
+        x_ref, _ = oracle.refine(ora_hand, obs, x_ref, rigid=REFINE_RIGID)
         x_ref, _, _ = oracle.pso_evolve(ora_hand, obs, x_ref, 32, 6, lb, ub, sd)
         cr = oracle.cal_cost(ora_hand, obs, x_ref)
         np.testing.assert_allclose(x_gpu, x_ref, rtol=0, atol=1e-6)
@@ -119,7 +120,7 @@ def test_pipelined_tracking_like_oracle(gh, oracle, ora_hand, np_hand, downsampl
         gh.ctx.check(rt.hpe_sync(gh.ctx.h))
         out = st.cpu().numpy()
         obs = oracle.preprocess(depth[f], downsample=downsample)
-        x_ref, _ = oracle.refine(ora_hand, obs, x_ref)
+        x_ref, _ = oracle.refine(ora_hand, obs, x_ref, rigid=REFINE_RIGID)
         x_ref, _, _ = oracle.pso_evolve(ora_hand, obs, x_ref, P, maxiter, lb, ub, sd)
         cr = oracle.cal_cost(ora_hand, obs, x_ref)
         np.testing.assert_allclose(out[:26], x_ref, rtol=0, atol=1e-6)
@@ -158,7 +159,7 @@ def test_sequence_tracking_like_oracle_and_per_frame(gh, oracle, ora_hand, np_ha
     x_ref = oracle_np.X0.copy()
     for f in range(n):
         obs = oracle.preprocess(depth[f])
-        x_ref, _ = oracle.refine(ora_hand, obs, x_ref)
+        x_ref, _ = oracle.refine(ora_hand, obs, x_ref, rigid=REFINE_RIGID)
         x_ref, _, _ = oracle.pso_evolve(ora_hand, obs, x_ref, P, maxiter, lb, ub, sd)
         cr = oracle.cal_cost(ora_hand, obs, x_ref)
         np.testing.assert_allclose(per_frame[f, :26], x_ref, rtol=0, atol=1e-6)
