@@ -93,6 +93,11 @@ def parse():
     ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
                     help="process group for --gpus N > 1 (nccl = RCCL over xGMI; gloo: the "
                          "per-frame exchange through host memory, a rehearsal mode)")
+    ap.add_argument("--exchange", default="frame",
+                    help="frame (default): the ranks' best is exchanged once per tracked frame "
+                         "(the reference's best-of-N, SURVEY.md §8e); gen:K additionally "
+                         "exchanges every K generations and injects the global best as an "
+                         "extra informant (ICP-PSO style, NOT the reference algorithm)")
     ap.add_argument("--same-device", action="store_true",
                     help="every rank uses cuda:0 (rehearse N ranks on a one-GPU box; with "
                          "--backend gloo)")
@@ -108,6 +113,13 @@ def parse():
     if a.frames_per_graph and not (a.resident and a.gpus == 1 and not a.dump):
         ap.error("--frames-per-graph needs --resident, one GPU and no --dump "
                  "(the per-frame exchange / dump sit between frames)")
+    a.exchange_every = 0
+    if a.exchange != "frame":
+        if not a.exchange.startswith("gen:") or not a.exchange[4:].isdigit() or int(a.exchange[4:]) < 1:
+            ap.error("--exchange takes frame or gen:K with K >= 1")
+        a.exchange_every = int(a.exchange[4:])
+        if a.frames_per_graph:
+            ap.error("--exchange gen:K runs without graph replay (no --frames-per-graph)")
     P, G, _ = CONFIGS[a.config]
     a.particles = a.particles or P
     a.generations = a.generations if a.generations is not None else G
@@ -381,7 +393,7 @@ def main():
     import torch.distributed as dist
     import hpe
     from hpe import synth
-    from hpe.dist import exchange_best, subswarm_seed
+    from hpe.dist import GenerationExchange, exchange_best, subswarm_seed
 
     if args.same_device:
         local = 0
@@ -426,6 +438,8 @@ def main():
     gathered = torch.zeros(world * 27, dtype=torch.float64, device=f"cuda:{local}")
     gathered_host = torch.zeros(world * 27, dtype=torch.float64)
     refine = 0 if args.no_refine else 1
+    gx = (GenerationExchange(ctx, args.exchange_every, args.backend)
+          if args.exchange_every else None)
 
     def step(f, ex=None):
         """One tracked frame; ex (diagnostic pass): gets the exchange's time in us."""
@@ -647,6 +661,9 @@ def main():
                                       {"seed": args.seed, "revert": TRAJ_REVERT,
                                        "frames": n_frames}),
                        "cloud_points": n_pts, "refine": bool(refine),
+                       "exchange": ("once per frame (best of N subswarms)" if not args.exchange_every
+                                    else f"every {args.exchange_every} generations + per frame "
+                                         "(ICP-PSO style, non-reference)"),
                        "parallelism": f"subswarms x{world}, all-gather best per frame"
                                       + ("" if world == 1 else f" ({args.backend}"
                                          + (", ranks sharing cuda:0)" if args.same_device
@@ -679,6 +696,10 @@ def main():
             line["vs_baseline_basis"] = ("cpu_baseline (BASELINE.md §2: no published number; "
                                          "the oracle on this box's host cores, same workload)")
         print(json.dumps(line), flush=True)
+    if gx is not None:
+        if gx.error is not None:
+            raise SystemExit(f"rank {rank}: generation exchange failed: {gx.error!r}")
+        gx.close()
     hand.ctx.close()
     if world > 1:
         dist.barrier()

@@ -428,7 +428,7 @@ __device__ __forceinline__ int dpp_i32(int v) {
 // Lexicographic (v, idx) minimum over the wave (Armadillo min(index): first minimum wins).
 // v must not be NaN.  Returns the winner's idx and payload in every lane.
 __device__ __forceinline__ void wave_argmin_lex(double v, int idx, int pay, int &out_idx,
-                                                int &out_pay) {
+                                                int &out_pay, double *out_min = nullptr) {
     double m = v;
     m = fmin(m, dpp_f64<0xB1>(m));
     m = fmin(m, dpp_f64<0x4E>(m));
@@ -436,6 +436,7 @@ __device__ __forceinline__ void wave_argmin_lex(double v, int idx, int pay, int 
     m = fmin(m, dpp_f64<0x140>(m));
     const double mn = fmin(fmin(readlane_f64(m, 0), readlane_f64(m, 16)),
                            fmin(readlane_f64(m, 32), readlane_f64(m, 48)));
+    if (out_min) *out_min = mn;
     int c = (v == mn) ? idx : 0x7fffffff;
     c = min(c, dpp_i32<0xB1>(c));
     c = min(c, dpp_i32<0x4E>(c));
@@ -451,13 +452,14 @@ __device__ __forceinline__ void wave_argmin_lex(double v, int idx, int pay, int 
 // The same over lanes 0..15 only (row 0; the other lanes are ignored): four DPP steps per
 // key inside the row and one readlane each, instead of the cross-row readlane chains.
 __device__ __forceinline__ void row0_argmin_lex(double v, int idx, int pay, int &out_idx,
-                                                int &out_pay) {
+                                                int &out_pay, double *out_min = nullptr) {
     double m = v;
     m = fmin(m, dpp_f64<0xB1>(m));
     m = fmin(m, dpp_f64<0x4E>(m));
     m = fmin(m, dpp_f64<0x141>(m));
     m = fmin(m, dpp_f64<0x140>(m));
     const double mn = readlane_f64(m, 0);
+    if (out_min) *out_min = mn;
     int c = (v == mn) ? idx : 0x7fffffff;
     c = min(c, dpp_i32<0xB1>(c));
     c = min(c, dpp_i32<0x4E>(c));
@@ -575,7 +577,10 @@ __device__ __forceinline__ void rigid_row(int r, double sz, double cz, double sy
 // MODE 0: rotation block (trig on lanes 0..2, Rg rows, Rg q + u); MODE 1: translation
 // block (P + u); MODE 2: store P = Rg q into Pout (u ignored, f untouched).
 enum RigidMode { RG_ROT = 0, RG_TRANS = 1, RG_STORE_P = 2 };
-template <int MODE, bool OUTLINE_TRIG = true>
+#ifndef HPE_RIGID_OUTLINE_TRIG
+#define HPE_RIGID_OUTLINE_TRIG 1
+#endif
+template <int MODE, bool OUTLINE_TRIG = HPE_RIGID_OUTLINE_TRIG>
 __device__ __forceinline__ void rigid_wave(FkSm &f, const RigidSm &R, double thl,
                                            SphXYZ *own = nullptr, double (*Pout)[3] = nullptr) {
     const int l = threadIdx.x & 63;
@@ -1056,7 +1061,8 @@ template <int MODE, int NT, bool FK = true, class CV>
 __device__ __forceinline__ double eval_block(Smem &sm, const DevObs &o, const CV &cv,
                                              const DevHand *__restrict__ H,
                                              int32_t *__restrict__ match, Pt pre,
-                                             int g_ts = BT_GENS, const SphXYZ *own_w0 = nullptr) {
+                                             int g_ts = BT_GENS, const SphXYZ *own_w0 = nullptr,
+                                             bool with_depth = true) {
     StampClock sc;
     sc.start();
     const int t = threadIdx.x;
@@ -1071,7 +1077,7 @@ __device__ __forceinline__ double eval_block(Smem &sm, const DevObs &o, const CV
     // wave 0 issues the depth gathers first (after the barrier: the other waves start
     // searching at once): their latency hides under the search
     DepthG dg{0.0, 0.0, 0.0, 0.f, false};
-    if (t < 64) dg = (FK || own_w0) ? depth_issue_at(own, t, o, H) : depth_issue(sm.fk, t, o, H);
+    if (t < 64 && with_depth) dg = (FK || own_w0) ? depth_issue_at(own, t, o, H) : depth_issue(sm.fk, t, o, H);
     // Waves 4..7 share the SIMDs with waves 0..3 and lose the age arbitration: they reached
     // the reduction ~0.5 us after waves 1..3.  Static priority for that half during the
     // search (MI355X_MICROARCH.md, two waves per SIMD, item 4).
@@ -1086,7 +1092,7 @@ __device__ __forceinline__ double eval_block(Smem &sm, const DevObs &o, const CV
     const bool coll = (MODE == EV_COST2_CORR || MODE == EV_COST2_FROZEN);
     double co = (coll && t < 144) ? collide_term(sm.fk, t, H) : 0.0;
     BLK_TS(g_ts, 8);
-    double dep = depth_finish(dg, o, t < HPE_NS);
+    double dep = depth_finish(dg, o, with_depth && t < HPE_NS);
     BLK_TS(g_ts, 9);
     if (HPE_STAMPS) asm volatile("" ::"v"(al), "v"(dep));
     WAVE_TS(g_ts, 16);

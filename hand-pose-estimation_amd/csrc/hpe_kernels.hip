@@ -236,6 +236,7 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_init(DevSwarm sw, const double *
         sw.pb[e] = x;
         sw.v[e] = 0.0;
     }
+    if (sw.ext && i == 0 && t == 0) sw.ext[HPE_DOF] = __builtin_inf();  // no candidate yet
     hand_put<HPE_NT>(sm.hand, hw);
     __syncthreads();
     const double c = eval_block<EV_COST, HPE_NT>(sm, o, cv, H, nullptr, pre);
@@ -250,10 +251,19 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_init(DevSwarm sw, const double *
 // load of the generation at once (own state, draws, sig[g-1] / gmin[g-1], both inboxes),
 // the topology decision, the informant, the velocity step and FK, with wave-level syncs
 // only.  Waves 1..3 prefetch the push links meanwhile; then all 8 waves search.
-__global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *__restrict__ og,
-                                                    const DevHand *__restrict__ Hg, int g,
-                                                    double W1, double C1, double C2,
-                                                    InboxCounts kin) {
+//
+// SPLIT > 1 (large clouds, k_pso_gen_split): SPLIT workgroups of NT threads carry one
+// particle -- blocks i, i + P, ... (the same XCD when P is a multiple of 8) -- each running
+// round 1, the velocity step and FK redundantly (the same operations on the same inputs:
+// the same bits) and searching its slice of the cloud; slice s's partial cost goes to
+// sw.part, and the last of the SPLIT to arrive (agent-scope release / acquire counter)
+// sums the partials in slice order and does pbest, gmin and the pushes.  More resident
+// waves per SIMD for a search of ~10^4 points than one 512-thread workgroup gives.
+template <int NT, int SPLIT>
+__device__ __forceinline__ void pso_gen_body(const DevSwarm &sw, const DevObs *__restrict__ og,
+                                             const DevHand *__restrict__ Hg, int g, double W1,
+                                             double C1, double C2, const InboxCounts &kin) {
+    static_assert(NT >= 256 && NT % 64 == 0, "waves 1..3 push, wave 0 carries the particle");
     BLK_TS(g, 0);
     // every argument word round 1 needs, loaded at entry as one batch: left alone the
     // compiler fetched g and the gmin / sig / link / bounds pointers in a second scalar
@@ -268,11 +278,13 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
     const DevObs o = *og;  // the selected frame (device-resident: graph-stable args)
     __shared__ Smem sm;
     __shared__ double ib[2][IB_KMAX][IB_FIELDS];
-    const int i = blockIdx.x + z0, t = threadIdx.x, P = sw.P, K = sw.K;
+    const int P = sw.P, K = sw.K;
+    const int i = (SPLIT == 1 ? (int)blockIdx.x : (int)blockIdx.x % P) + z0, t = threadIdx.x;
+    const int slice = SPLIT == 1 ? 0 : (int)blockIdx.x / P;
     // valid slots of this receiver's kept (0) / rebuilt (1) inbox: only these are read
     // (read at blockIdx.x, clamped, unconditionally: the address depends on no loaded
     // argument, so these loads leave with the argument loads instead of after them)
-    const int kb = (int)blockIdx.x & (KIN_MAX - 1);
+    const int kb = (SPLIT == 1 ? (int)blockIdx.x : i) & (KIN_MAX - 1);
     const int k0r = kin.k0[kb], k1r = kin.k1[kb];
     const int k0 = (P <= KIN_MAX) ? k0r : K, k1 = (P <= KIN_MAX) ? k1r : K;
     // Round 1: every load of the generation is issued before any value is used (one
@@ -280,10 +292,14 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
     // (waves 1..7); own state, own pbest cost, inbox tags / costs, gmin cells, sig (wave 0).
     // staged into LDS before the first barrier (after the argument batch: issued ahead of
     // it, this load made the compiler wait for the first argument words alone)
-    const double hw = hand_word<HPE_NT>((const DevHand *)((const char *)Hg + z0));
+    const double hw = hand_word<NT>((const DevHand *)((const char *)Hg + z0));
     const DevHand *__restrict__ H = &sm.hand;
     sc.lap(4);
-    const CloudGlobal cv = obs_cloud(o);
+    CloudGlobal cv = obs_cloud(o);
+    if (SPLIT > 1) {  // this block's slice of the cloud
+        const int per = (o.n + SPLIT - 1) / SPLIT, s0 = min(slice * per, o.n);
+        cv = CloudGlobal{cv.cx + s0, cv.cy + s0, cv.cz + s0, min(s0 + per, o.n) - s0};
+    }
     const Pt pre = load_pt(cv, t);  // this thread's first cloud point, used after FK
     const size_t e = (size_t)i * HPE_DOF + t;
     const int q = t - 64;  // pushing lanes (waves 1..3): var-1 links now, var-0 after the decision
@@ -291,16 +307,19 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
     double pbi = 0, xo = 0, vo = 0, rp = 0, rg = 0;  // own state (lanes t < 26 of wave 0)
     double lbt = 0, ubt = 0;                          // bounds of dimension t
     int inf = 0, islot = -1, var = 0;
+    double exr = 0.0;       // per-generation exchange (sw.ext): the candidate's row, lane t
+    bool use_ext = false;   // ... and whether it beats this particle's informant
     if (t >= 64) {
         // ---- waves 1..7: both informant inboxes (payload rows) into LDS
         // the k0 valid kept slots, then the k1 valid rebuilt ones
         const double *src = sw.inbox + ib_index(sw, (g - 1) & 1, 0, i, 0);
         const size_t var_stride = (size_t)P * K * IB_FIELDS;
         const int n = (k0 + k1) * IB_FIELDS, u0 = t - 64;
-        double a[3];
+        constexpr int NL = (2 * IB_KMAX * IB_FIELDS + NT - 65) / (NT - 64);  // loads per lane
+        double a[NL];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {  // unconditional (clamped) loads: no early wait
-            const int u = min(u0 + k * (HPE_NT - 64), max(n - 1, 0));
+        for (int k = 0; k < NL; ++k) {  // unconditional (clamped) loads: no early wait
+            const int u = min(u0 + k * (NT - 64), max(n - 1, 0));
             const int vr = u >= k0 * IB_FIELDS ? 1 : 0;
             a[k] = src[vr * var_stride + (u - vr * k0 * IB_FIELDS)];
         }
@@ -309,8 +328,8 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
             sm.draws[j] = philox_u01(sw.seed, j < HPE_DOF ? ST_RP : ST_RG, g, i, d);
         }
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const int u = u0 + k * (HPE_NT - 64);
+        for (int k = 0; k < NL; ++k) {
+            const int u = u0 + k * (NT - 64);
             if (u < n) (&ib[0][0][0])[(u >= k0 * IB_FIELDS ? IB_KMAX * IB_FIELDS - k0 * IB_FIELDS : 0) + u] = a[k];
         }
     } else {
@@ -332,6 +351,7 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
         }
         const unsigned long long gcell = gmin_load(sw, g - 1);
         const Sig pv = sw.sig[g > 1 ? g - 1 : 0];
+        if (sw.ext) exr = sw.ext[t <= HPE_DOF ? t : HPE_DOF];
         const double fmin = gmin_reduce(gcell);  // NaN when no value was written
         // informant = first argmin of pbest cost over {i} U incoming (PSO.cpp:810-812),
         // under BOTH variants while the gmin reduction is in flight (independent chains):
@@ -340,6 +360,7 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
         // row) or 63.
         const int self_lane = (K <= 15) ? 15 : 63;
         int infv[2], islv[2];
+        double infc[2];
 #pragma unroll
         for (int vr = 0; vr < 2; ++vr) {
             const long long tag = __double_as_longlong(tg[vr]);
@@ -349,8 +370,8 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
             double v = ok ? tc[vr] : (self ? pci : __builtin_inf());
             const int idx = ok ? (int)(tag & 0xffffffff) : (self ? i : 0x7fffffff);
             if (v != v) v = __builtin_inf();
-            if (K <= 15) row0_argmin_lex(v, idx, ok ? t : -1, infv[vr], islv[vr]);
-            else wave_argmin_lex(v, idx, ok ? t : -1, infv[vr], islv[vr]);
+            if (K <= 15) row0_argmin_lex(v, idx, ok ? t : -1, infv[vr], islv[vr], &infc[vr]);
+            else wave_argmin_lex(v, idx, ok ? t : -1, infv[vr], islv[vr], &infc[vr]);
         }
         BLK_TS(g, 6);
         // end-of-generation update of g-1 (PSO.cpp:864-877) / initial gbest (:755-760),
@@ -367,7 +388,7 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
             sg.topo = pv.topo;
         }
         if (sg.count > 0) sg.topo = g;  // topology rebuilt when count > 0 (PSO.cpp:790)
-        if (i == 0 && t == 0) sw.sig[g] = sg;
+        if (i == 0 && slice == 0 && t == 0) sw.sig[g] = sg;
         if (t == 0) {
             sm.iscal[0] = sg.topo;
             sm.dscal[4] = pci;
@@ -377,11 +398,13 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
         sc.lap(0);
         inf = var ? infv[1] : infv[0];
         islot = var ? islv[1] : islv[0];
+        // the exchanged candidate (index "P": after every local one) wins only strictly
+        if (sw.ext) use_ext = readlane_f64(exr, HPE_DOF) < (var ? infc[1] : infc[0]);
         if (t < HPE_DOF) sm.pbr[t] = pbi;  // for the pushing waves, if x does not improve
         BLK_TS(g, 7);
         sc.lap(1);
     }
-    hand_put<HPE_NT>(sm.hand, hw);
+    hand_put<NT>(sm.hand, hw);
     BLK_TS(g, 1);
     __syncthreads();  // informant rows and draws in LDS
     SphXYZ own0{0.0, 0.0, 0.0};  // wave 0: the centres FK leaves in registers
@@ -393,18 +416,20 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
             rp = sm.draws[t];
             rg = sm.draws[HPE_DOF + t];
             double vn;
-            if (inf == i) {
+            if (inf == i && !use_ext) {
                 vn = W1 * vo + (C1 * rp) * (pbi - xo);
             } else {
-                const double pbn = ib[var][islot][2 + t];
+                const double pbn = use_ext ? exr : ib[var][islot][2 + t];
                 vn = (W1 * vo + (C1 * rp) * (pbi - xo)) + (C2 * rg) * (pbn - xo);
             }
             double xn = xo + vn;
             const double xr = xn;
             if (xr < lbt) { xn = lbt; vn = 0.; }
             if (xr > ubt) { xn = lbt; vn = 0.; }  // above max -> MIN (PSO.cpp:372)
-            sw.v[e] = vn;
-            sw.xh[(size_t)g * P * HPE_DOF + e] = xn;
+            if (slice == 0) {  // (every slice computes the same x, v)
+                sw.v[e] = vn;
+                sw.xh[(size_t)g * P * HPE_DOF + e] = xn;
+            }
             sm.fk.th[t] = xn;
             thl = xn;
         }
@@ -419,8 +444,34 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
     const double pci = sm.dscal[4];
     const Link lk0 = load_link(sw, g, i, q, topo, q >= 3 * IB_FIELDS);
     // ---- evaluation and pbest (PSO.cpp:848-861)
-    const double fx = eval_block<EV_COST, HPE_NT, false>(sm, o, cv, H, nullptr, pre, g, &own0);
+    double fx = eval_block<EV_COST, NT, false>(sm, o, cv, H, nullptr, pre, g, &own0, slice == 0);
     BLK_TS(g, 4);
+    if (SPLIT > 1) {
+        // slice totals in sw.part; the last block of the particle to arrive adds them in
+        // slice order (deterministic) and carries on; the others are done.  Release: the
+        // partial drained, agent fence, counter; acquire: one lane, then the barrier.
+        __shared__ int last_blk;
+        if (t == 0) {
+            double *pp = sw.part + ((size_t)(g & 1) * P + i) * SPLIT;
+            unsigned *ctr = sw.arrive + (size_t)(g & 1) * P + i;
+            pp[slice] = fx;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            const unsigned prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const bool last = prev == SPLIT - 1;
+            if (last) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                double tot = 0.0;
+#pragma unroll
+                for (int k = 0; k < SPLIT; ++k) tot += pp[k];
+                *ctr = 0u;  // next used two generations on, after kernel boundaries
+                sm.dscal[6] = tot;
+            }
+            last_blk = last ? 1 : 0;
+        }
+        __syncthreads();
+        if (!last_blk) return;
+        fx = sm.dscal[6];
+    }
     sc.start();
     const bool better = fx < pci;
     const double pn = better ? fx : pci;
@@ -437,6 +488,26 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
     BLK_TS(g, 5);
     sc.lap(3);
     sc.span(5);
+}
+
+__global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *__restrict__ og,
+                                                    const DevHand *__restrict__ Hg, int g,
+                                                    double W1, double C1, double C2,
+                                                    InboxCounts kin) {
+    pso_gen_body<HPE_NT, 1>(sw, og, Hg, g, W1, C1, C2, kin);
+}
+
+// Large clouds (N > RF_STAGE_MAX, e.g. the full ~9.3k-point cloud): SPLIT workgroups of 256
+// threads per particle, three resident per CU (<= 168 VGPRs).
+#define PSO_SPLIT 3
+#define PSO_SPLIT_NT 256
+template <int SPLIT>
+__global__ __launch_bounds__(PSO_SPLIT_NT, 3) void k_pso_gen_split(DevSwarm sw,
+                                                                  const DevObs *__restrict__ og,
+                                                                  const DevHand *__restrict__ Hg,
+                                                                  int g, double W1, double C1,
+                                                                  double C2, InboxCounts kin) {
+    pso_gen_body<PSO_SPLIT_NT, SPLIT>(sw, og, Hg, g, W1, C1, C2, kin);
 }
 
 // ---------------------------------------------------------------- wave-per-particle form
@@ -497,6 +568,7 @@ __global__ __launch_bounds__(PW_NT) void k_pso_init_w(DevSwarm sw, const double 
     const CloudGlobal cv = obs_cloud(o);
     const Pt pre = load_pt(cv, l);
     const double *sd = sw.bounds + 2 * HPE_DOF;
+    if (sw.ext && blockIdx.x == 0 && t == 0) sw.ext[HPE_DOF] = __builtin_inf();  // no candidate yet
     if (l < HPE_DOF) {  // particles = x0 + randn % std (PSO.cpp:67-72)
         const size_t e = (size_t)ic * HPE_DOF + l;
         const double x = x0[l] + sw.normals[e] * sd[l];
@@ -560,6 +632,7 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
     }
     const unsigned long long gcell = gmin_load(sw, g - 1);
     const Sig pv = sw.sig[g > 1 ? g - 1 : 0];
+    const double exr = sw.ext ? sw.ext[l <= HPE_DOF ? l : HPE_DOF] : 0.0;  // exchange (sw.ext)
     // the draws while the loads are in flight
     const int dl = l < HPE_DOF ? l : 0;
     const double rp = philox_u01(sw.seed, ST_RP, g, ic, dl);
@@ -597,15 +670,17 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
     }
     if (v != v) v = __builtin_inf();
     int inf, islot;
-    if (K <= 15) row0_argmin_lex(v, idx, slot, inf, islot);
-    else wave_argmin_lex(v, idx, slot, inf, islot);
+    double infc;
+    if (K <= 15) row0_argmin_lex(v, idx, slot, inf, islot, &infc);
+    else wave_argmin_lex(v, idx, slot, inf, islot, &infc);
+    const bool use_ext = sw.ext && readlane_f64(exr, HPE_DOF) < infc;  // strictly better
     // ---- velocity, position, check_constraints (PSO.cpp:824-842, 358-377)
     if (l < HPE_DOF) {
         double vn;
-        if (inf == ic) {
+        if (inf == ic && !use_ext) {
             vn = W1 * vo + (C1 * rp) * (pbi - xo);
         } else {
-            const double pbn = sw.inbox[ib_index(sw, (g - 1) & 1, var, ic, islot) + 2 + l];
+            const double pbn = use_ext ? exr : sw.inbox[ib_index(sw, (g - 1) & 1, var, ic, islot) + 2 + l];
             vn = (W1 * vo + (C1 * rp) * (pbi - xo)) + (C2 * rg) * (pbn - xo);
         }
         double xn = xo + vn;
@@ -642,6 +717,26 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
         const int q = l + 64 * k;
         push_inbox_w(sw, g, i, q, lk[k], q < 3 * IB_FIELDS ? g + 1 : topo, pn, f.th);
     }
+}
+
+// The opt-in per-generation exchange (hpe_set_exchange): this subswarm's best after
+// generation g -- {pbest row, pbest cost} of the first argmin of the generation's pbest
+// costs (NaN as +inf, as the informant choice) -- into sw.ext, which the caller's
+// collective then replaces by the best over all subswarms.  One workgroup.
+__global__ __launch_bounds__(HPE_NT) void k_swarm_best(DevSwarm sw, int g) {
+    __shared__ Smem sm;
+    const int t = threadIdx.x, P = sw.P;
+    VI mine = {__builtin_inf(), 0};
+    for (int k = t; k < P; k += HPE_NT) {
+        const double v = nan_inf(sw.pch[(size_t)g * P + k]);
+        if (v < mine.v) {
+            mine.v = v;
+            mine.i = k;
+        }
+    }
+    const VI b = block_argmin(sm, mine);
+    if (t < HPE_DOF) sw.ext[t] = sw.pb[(size_t)b.i * HPE_DOF + t];
+    if (t == HPE_DOF) sw.ext[HPE_DOF] = sw.pch[(size_t)g * P + b.i];
 }
 
 // u64 wave helpers of k_pso_final's replay: lane l - 1's value (lane 0: fill), the
@@ -692,8 +787,12 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
                                                       int same_eval = 0,
                                                       unsigned long long *__restrict__ seq_dev = nullptr,
                                                       unsigned long long *done_host = nullptr,
-                                                      double *__restrict__ hist = nullptr) {
+                                                      double *__restrict__ hist = nullptr,
+                                                      const int *__restrict__ fail = nullptr) {
     constexpr int CH = 2048;  // generations staged per pass
+    // a timed-out multi-workgroup refine (DevMw::err, set until the host has reported it):
+    // this frame's result is undefined, so bestp and cost become NaN
+    const int failed = (TAIL && fail) ? __hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
     __shared__ Smem sm;
     __shared__ double gm[CH];
     __shared__ int tp[CH];
@@ -849,6 +948,13 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
     for (int c = t; c < (G + 1) * GMIN_SHARDS; c += HPE_NT) sw.gmin[(size_t)c * GMIN_STRIDE] = ~0ull;
     if (TAIL) {
         if (obs_out && t < (int)(sizeof(DevObs) / 8)) ((unsigned long long *)obs_out)[t] = obs_word;
+        if (failed) {
+            if (t <= HPE_DOF) {
+                out[t] = __builtin_nan("");
+                if (hist) hist[t] = __builtin_nan("");
+            }
+            return;
+        }
         if (same_eval && last >= 0) return;  // out[26] = gcost = cal_cost(bestp)
         const DevObs o = *og;
         if (t < HPE_DOF) sm.fk.th[t] = bp;
@@ -888,6 +994,11 @@ struct __align__(16) RefineSm {
     double x0[32];
     double f[RF_NW];
     double fg[RF_NW];  // the gradient points' costs (k_refine, single-workgroup form)
+    // the speculated Goldstein nodes' own decisions (gold_decide): byte w = node w's code
+    // (0 down, 1 up, 2 accept), gpost[w] = its bracket {a, b, alpha} after the decision
+    // and its own alpha
+    unsigned long long gcode;
+    double gpost[RF_NW][4];
     FkX X;  // rotation-only joint terms of x0 (refine block 2: translation steps)
     RigidSm rg;  // hand-frame centres, block 2's rotated centres, collision (rigid refine)
     unsigned ts_n;  // diagnostic build: refine timeline entries written
@@ -902,6 +1013,40 @@ __device__ __forceinline__ void gold_up(double &a, double b, double &alpha) {
 __device__ __forceinline__ void gold_down(double a, double &b, double &alpha) {
     b = alpha;
     alpha = 0.5 * (a + alpha);
+}
+
+// A speculated node's Goldstein test (PSO.cpp:459-474), taken by the node's own wave right
+// after its evaluation with the same operations the serial search applies at that node
+// (its bracket state replayed from the round's start): the walk then follows byte codes
+// and reads one post-state instead of redoing the fp64 tests level by level.
+struct GoldIn {
+    double fk, gp;  // f_k and g'p of the search
+    double a, b, al;  // this node's bracket state before its test (al = its alpha)
+};
+__device__ __forceinline__ void gold_decide(unsigned long long *codes, double (*post)[4], int w,
+                                            double f1, const GoldIn &g) {
+    const double armijo = g.fk + 0.25 * g.al * g.gp;
+    const double gold = g.fk + (1 - 0.25) * g.al * g.gp;
+    double a = g.a, b = g.b, alpha = g.al;
+    unsigned code;
+    if (f1 <= armijo) {
+        if (f1 >= gold) {
+            code = 2;
+        } else {
+            code = 1;
+            gold_up(a, b, alpha);
+        }
+    } else {
+        code = 0;
+        gold_down(a, b, alpha);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        ((unsigned char *)codes)[w] = (unsigned char)code;
+        post[w][0] = a;
+        post[w][1] = b;
+        post[w][2] = alpha;
+        post[w][3] = g.al;
+    }
 }
 
 // ---------------------------------------------------------------- multi-workgroup refine
@@ -989,12 +1134,14 @@ __device__ __forceinline__ double mw_sum(const MwLeader &ml, int w) {
 // own rs.w[w].th.  Ends with a workgroup barrier.
 // RIGID: the nodes' spheres by rigid_wave (rblk 0: rotation block, 1: translation block),
 // the collision the constant rs.rg.C.
+// gin (Goldstein nodes): each node wave also takes its own test (gold_decide).
 template <bool MW, bool RIGID = false, class CV>
 __device__ __forceinline__ void eval_nodes(RefineSm &rs, int nn, const DevObs &o, const CV &cv,
                                            const DevHand *__restrict__ H,
                                            const int32_t *__restrict__ match, FkX *Xt,
                                            MwLeader *ml, int *flag, const double *thr = nullptr,
-                                           const FrozenPts *fp = nullptr, int rblk = 0) {
+                                           const FrozenPts *fp = nullptr, int rblk = 0,
+                                           const GoldIn *gin = nullptr) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     if (!MW) {
         if (w < nn) {
@@ -1008,6 +1155,7 @@ __device__ __forceinline__ void eval_nodes(RefineSm &rs, int nn, const DevObs &o
                 f = eval_wave_frozen<true>(rs.w[w], o, cv, H, match, Xt, thr, fp);
             }
             if (l == 0) rs.f[w] = f;
+            if (gin) gold_decide(&rs.gcode, rs.gpost, w, f, *gin);
         }
         REF_TS(rs.ts_n, 9);  // wave 0's node done
         __syncthreads();
@@ -1036,7 +1184,9 @@ __device__ __forceinline__ void eval_nodes(RefineSm &rs, int nn, const DevObs &o
     if (w < nn) {
         const double al = mw_sum(*ml, w);
         const double f = RIGID ? (al * o.lambda + dep) + rs.rg.C : (al * o.lambda + dep) + co;
-        if (l == 0) rs.f[w] = ml->failed ? __builtin_nan("") : f;
+        const double fr = ml->failed ? __builtin_nan("") : f;
+        if (l == 0) rs.f[w] = fr;
+        if (gin) gold_decide(&rs.gcode, rs.gpost, w, fr, *gin);
     }
     __syncthreads();
 }
@@ -1243,19 +1393,23 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
         const GoldShape sh = gold_shape<POL>(ctx);
         const int nn = sh.n;
         double thl = 0.0;  // theta[l] of this wave's node (FK's trig reads it in a register)
+        GoldIn gin{fk, gp, A, B, alpha};
         if (w < nn) {
-            double a = A, b = B, al2 = alpha;
             const int nbw = (int)((sh.nb >> (8 * w)) & 0xff), len = nbw >> 5, bits = nbw & 31;
             for (int k = 0; k < len; ++k) {
-                if ((bits >> k) & 1) gold_up(a, b, al2);
-                else gold_down(a, b, al2);
+                if ((bits >> k) & 1) gold_up(gin.a, gin.b, gin.al);
+                else gold_down(gin.a, gin.b, gin.al);
             }
-            thl = rs.x0[l < HPE_DOF ? l : 0] + al2 * pl;
+            thl = rs.x0[l < HPE_DOF ? l : 0] + gin.al * pl;
             if (l < HPE_DOF) rs.w[w].th[l] = thl;
         }
-        eval_nodes<MW, RIGID>(rs, nn, o, cv, H, match, Xt, ml, flag, &thl, fp, rblk);
+        eval_nodes<MW, RIGID>(rs, nn, o, cv, H, match, Xt, ml, flag, &thl, fp, rblk, &gin);
         if (MW && ml->failed) break;  // the launch is ending early (DevMw::err)
-        int node = 0;
+        // the walk: every node took its own test (gold_decide), so the serial search's path
+        // through the shape is a chain of byte codes; the bracket state after the round is
+        // the post-state of the last node tested
+        const unsigned long long codes = rs.gcode;
+        int node = 0, lastn = -1;
         accepted = -1;
 #pragma unroll
         for (int lev = 0; lev < 6; ++lev) {  // the deepest shape path is 6 nodes
@@ -1266,27 +1420,28 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
                 break;
             }
             ++it;
-            const double f1 = rs.f[node];
-            const double armijo = fk + 0.25 * alpha * gp;
-            const double gold = fk + (1 - 0.25) * alpha * gp;
-            if (f1 <= armijo) {
-                if (f1 >= gold) {
-                    tk = alpha;
-                    done = true;
-                    accepted = node;
-                } else {
-                    gold_up(A, B, alpha);
-                    node = (int)((sh.up >> (4 * node)) & 15u);
-                    ctx = 2;
-                    if (HPE_STAMPS) path |= 1ull << (it - 1);
-                    if (HPE_STAMPS && blockIdx.x == 0 && t == 0) hpe_stamps[8] += 1;
-                }
+            const unsigned code = (unsigned)(codes >> (8 * node)) & 0xffu;
+            lastn = node;
+            if (code == 2) {
+                done = true;
+                accepted = node;
+            } else if (code == 1) {
+                node = (int)((sh.up >> (4 * node)) & 15u);
+                ctx = 2;
+                if (HPE_STAMPS) path |= 1ull << (it - 1);
+                if (HPE_STAMPS && blockIdx.x == 0 && t == 0) hpe_stamps[8] += 1;
             } else {
-                gold_down(A, B, alpha);
                 node = (int)((sh.dn >> (4 * node)) & 15u);
                 ctx = 1;
                 if (HPE_STAMPS && blockIdx.x == 0 && t == 0) hpe_stamps[7] += 1;
             }
+        }
+        if (accepted >= 0) {
+            tk = rs.gpost[accepted][3];
+        } else if (lastn >= 0 && !done) {
+            A = rs.gpost[lastn][0];
+            B = rs.gpost[lastn][1];
+            alpha = rs.gpost[lastn][2];
         }
         if (!done && it >= 30) done = true;  // tk stays 0
         // x0 is read only before eval_nodes' barrier in a round

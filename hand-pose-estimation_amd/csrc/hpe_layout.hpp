@@ -74,6 +74,14 @@ struct DevSwarm {
     double *gpos;             // 26               gbest position (final)
     double *trace_g;          // [G]
     int *trace_count, *trace_topo;
+    // opt-in per-generation exchange (hpe_set_exchange; NOT the reference's algorithm):
+    // {pose[26], cost} of the best pbest over all subswarms at the last exchange, an extra
+    // informant candidate of every particle; nullptr: off (the reference's swarm)
+    double *ext;
+    // large clouds (k_pso_gen_split): slice partial costs [2][P][PSO_SPLIT] and arrival
+    // counters [2][P] by generation parity
+    double *part;
+    unsigned *arrive;
     uint64_t seed;
     int P, G, K;
 };

@@ -64,6 +64,7 @@ SIGNATURES = {
     "hpe_pso_trace": (C.c_int, [C.c_void_p, dp, ip, ip, C.c_int]),
     "hpe_refine_init_pose": (C.c_int, [C.c_void_p, dp, ip]),
     "hpe_set_refine_exact": (C.c_int, [C.c_void_p, C.c_int]),
+    "hpe_set_exchange": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]),
     "hpe_get_refine_exact": (C.c_int, [C.c_void_p]),
     "hpe_track_frame": (C.c_int, [C.c_void_p, C.c_int, C.c_int, dp, dp]),
     "hpe_track_frame_dev": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
@@ -76,6 +77,9 @@ SIGNATURES = {
     "hpe_render_depth": (C.c_int, [C.c_void_p, dp, C.c_double, fp]),
     "hpe_debug_stamps": (C.c_int, [C.POINTER(C.c_uint64)]),
 }
+
+# hpe_exchange_fn: int (*)(void *user, double *d_ext, int generation)
+EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_int)
 
 _lib = None
 

@@ -7,6 +7,10 @@ all-gather + argmin rather than all-reduce; 216 B per rank, latency-bound.
 Because gbest never enters the reference velocity update (PSO.cpp:824-832), exchanging
 once per frame is exactly "best of N independent swarms"; the winner becomes every
 rank's next-frame x0 (testmodel.cpp:138).
+
+GenerationExchange adds the opt-in ICP-PSO style exchange (NOT the reference algorithm):
+every K generations each rank's best pbest is all-gathered and the best over all ranks
+becomes an extra informant candidate of every particle (hpe_set_exchange).
 """
 from __future__ import annotations
 
@@ -41,3 +45,57 @@ def exchange_best(state: torch.Tensor, gathered: torch.Tensor | None = None,
     dist.all_gather_into_tensor(gathered, state, group=group)
     state.copy_(pick_best(gathered.view(world, STATE_LEN)))
     return state
+
+
+class GenerationExchange:
+    """The opt-in per-generation exchange (hpe_set_exchange; ICP-PSO style, labelled
+    non-reference: the reference's gbest never enters the velocity, PSO.cpp:824-832).
+
+    After every `every`-th generation the library writes this rank's best pbest
+    {pose, cost} into `ext` (27 doubles on the context's device) and calls back here; the
+    callback replaces it by the best over all ranks (exchange_best: all-gather + lowest
+    cost, ties to the lowest rank) ON THE CONTEXT'S STREAM, so the next generation reads it
+    without a host synchronisation (nccl = RCCL).  backend "gloo" (a rehearsal: several
+    ranks on one GPU) goes through host memory and synchronises the stream.  Keep the
+    object alive while the context tracks; close() turns the exchange off."""
+
+    def __init__(self, ctx, every: int, backend: str = "nccl", group=None):
+        import ctypes as C
+
+        from . import _lib
+        self.ctx, self.every, self.backend, self.group = ctx, every, backend, group
+        dev = torch.device("cuda", ctx.device)
+        world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.ext = torch.zeros(STATE_LEN, dtype=torch.float64, device=dev)
+        self.gathered = torch.zeros(world * STATE_LEN, dtype=torch.float64,
+                                    device=dev if backend == "nccl" else "cpu")
+        self.stream = torch.cuda.ExternalStream(ctx.lib.hpe_stream(ctx.h), device=dev)
+        self.calls = 0
+        self.error = None
+        self._cb = _lib.EXCHANGE_FN(self._call)  # referenced for the context's lifetime
+        ctx.check(ctx.lib.hpe_set_exchange(ctx.h, every, C.c_void_p(self.ext.data_ptr()),
+                                           C.cast(self._cb, C.c_void_p), None))
+
+    def _call(self, user, d_ext, generation):
+        try:
+            if not dist.is_initialized() or dist.get_world_size(self.group) == 1:
+                pass  # one swarm: its own best is the candidate
+            elif self.backend == "nccl":
+                with torch.cuda.stream(self.stream):
+                    exchange_best(self.ext, self.gathered, self.group)
+            else:
+                self.stream.synchronize()
+                h = self.ext.cpu()
+                exchange_best(h, self.gathered, self.group)
+                with torch.cuda.stream(self.stream):
+                    self.ext.copy_(h)
+            self.calls += 1
+            return 0
+        except Exception as e:  # noqa: BLE001 -- reported through the C ABI's status
+            self.error = e
+            return 1
+
+    def close(self):
+        if self.ctx is not None and self.ctx.h:
+            self.ctx.check(self.ctx.lib.hpe_set_exchange(self.ctx.h, 0, None, None, None))
+        self.ctx = None

@@ -150,6 +150,20 @@ int hpe_set_seed(hpe_ctx *ctx, uint64_t seed);
 int hpe_pso_evolve(hpe_ctx *ctx, const double x0[26], int num_p, double bestp[26],
                    double *bestcost_out);
 
+/* Opt-in per-generation exchange between subswarms (ICP-PSO style; NOT the reference's
+ * algorithm, whose gbest never enters the velocity, PSO.cpp:824-832).  every > 0: after
+ * every `every`-th generation g < maxiter-1 of each pso_evolve of this context (standalone
+ * or inside a tracking call) the library writes this subswarm's best pbest {pose[26], cost}
+ * into d_ext (27 doubles of caller-owned device memory), then calls
+ * fn(user, d_ext, g), which must enqueue on hpe_stream(ctx) the collective that replaces
+ * d_ext by the best over all subswarms (lowest cost, ties to the lowest rank) and return
+ * 0.  From generation g + 1 on, d_ext is an extra informant candidate of every particle:
+ * it replaces the particle's informant when its cost is strictly lower (PSO.cpp:807-832 with
+ * one more candidate, ranked after the local ones).  Tracking calls run without graph
+ * replay while it is on.  every = 0 turns it off (fn, user, d_ext ignored). */
+typedef int (*hpe_exchange_fn)(void *user, double *d_ext, int generation);
+int hpe_set_exchange(hpe_ctx *ctx, int every, double *d_ext, hpe_exchange_fn fn, void *user);
+
 /* Per-generation trace of the last pso_evolve (debug / parity):
  * gbest cost, stagnation count, topology generation; arrays of maxiter-1. */
 int hpe_pso_trace(hpe_ctx *ctx, double *gbest, int32_t *count, int32_t *topo, int n);
@@ -226,7 +240,7 @@ int hpe_track_pipelined(hpe_ctx *ctx, int num_p, int refine, double *d_state,
 #define HPE_PROF_PREP 4      /* k_preprocess (hpe_prepare_frame, preprocessing stream) */
 #define HPE_PROF_OPT_DESCENT 5 /* k_opt_descent: pso_optimise descent phase */
 #define HPE_PROF_OPT_MOVE 6    /* k_opt_move: pso_optimise velocity / cost phase */
-/* 7: reserved (the grid-resident generation loop of rounds 1-2, removed) */
+#define HPE_PROF_SWARM_BEST 7 /* k_swarm_best: a subswarm's best for the per-generation exchange */
 #define HPE_PROF_KERNELS 8
 int hpe_profile_enable(hpe_ctx *ctx, int on);
 int hpe_profile_read(hpe_ctx *ctx, int32_t *launches, double *total_ms, double *min_ms,

@@ -444,117 +444,207 @@ static void check_constraints(double *x, double *v, const double *lb, const doub
     }
 }
 
-/* pso_evolve, PSO.cpp:717-886 */
+/* pso_evolve, PSO.cpp:717-886, as a swarm state advanced one generation at a time (the
+ * multi-subswarm mirror below steps several in lockstep). */
+typedef struct {
+    int P;
+    uint64_t seed;
+    double *x, *v, *pb, *pc, *fx;
+    int *links, *in_off, *in_src, *fill;
+    double gpos[26], gcost;
+    int count, topo;
+} ora_swarm;
+
+static void swarm_free(ora_swarm *s) {
+    free(s->x); free(s->v); free(s->pb); free(s->pc); free(s->fx);
+    free(s->links); free(s->in_off); free(s->in_src); free(s->fill);
+}
+
+static void swarm_init(ora_swarm *s, const ora_hand *h, const ora_obs *o, const double x0[26],
+                       int P, const double stdv[26], uint64_t seed, ora_pso_trace *trace,
+                       int nthreads) {
+    const int D = ORA_DOF;
+    s->P = P;
+    s->seed = seed;
+    s->x = (double *)calloc((size_t)D * P, sizeof(double));
+    s->v = (double *)calloc((size_t)D * P, sizeof(double));
+    s->pb = (double *)calloc((size_t)D * P, sizeof(double));
+    s->pc = (double *)calloc((size_t)P, sizeof(double));
+    s->fx = (double *)calloc((size_t)P, sizeof(double));
+    s->links = (int *)calloc((size_t)3 * P, sizeof(int));
+    s->in_off = (int *)calloc((size_t)P + 1, sizeof(int));
+    s->in_src = (int *)calloc((size_t)3 * P, sizeof(int));
+    s->fill = (int *)calloc((size_t)P, sizeof(int));
+    s->gcost = 1e100;
+    memset(s->gpos, 0, sizeof(s->gpos));
+    /* generate_particles, PSO.cpp:56-74 */
+    ora_normals(seed, P, s->x);
+    for (int i = 0; i < P; ++i)
+        for (int d = 0; d < D; ++d) s->x[D * i + d] = x0[d] + s->x[D * i + d] * stdv[d];
+    memcpy(s->pb, s->x, sizeof(double) * D * P);
+    ora_eval_costs(h, o, s->x, P, 0, s->pc, nthreads); /* PSO.cpp:748-763 */
+    if (trace && trace->pcost0) memcpy(trace->pcost0, s->pc, sizeof(double) * P);
+    for (int i = 0; i < P; ++i) /* serial semantics of the racy init update */
+        if (s->pc[i] < s->gcost) {
+            s->gcost = s->pc[i];
+            memcpy(s->gpos, s->x + D * i, sizeof(s->gpos));
+        }
+    s->count = 100; /* :768 */
+    s->topo = -1;
+}
+
+/* One generation g >= 1 (iter g + 1 of PSO.cpp:778-880).  ext (the opt-in exchange, NULL
+ * in the reference): {pose, cost} of the exchanged best, an extra informant candidate
+ * ranked after the local ones. */
+static void swarm_gen(ora_swarm *s, const ora_hand *h, const ora_obs *o, int g,
+                      const double lb[26], const double ub[26], const double *ext,
+                      ora_pso_trace *trace, int nthreads) {
+    const int D = ORA_DOF, P = s->P;
+    const uint64_t seed = s->seed;
+    const double W1 = 1. / (2 * log(2.0)), C1 = 0.5 + log(2.0), C2 = C1; /* :772-774 */
+    if (s->count > 0) { /* topology rebuild, :790-803 */
+        for (int q = 0; q < P; ++q)
+            for (int k = 0; k < 3; ++k) {
+                const double u = ora_u01(seed, ST_LINK, (uint32_t)g, (uint32_t)q, (uint32_t)k);
+                s->links[3 * q + k] = (int)floor(u * (P - 1) + 0.5);
+            }
+        memset(s->in_off, 0, sizeof(int) * (P + 1));
+        for (int e = 0; e < 3 * P; ++e) s->in_off[s->links[e] + 1]++;
+        for (int i = 0; i < P; ++i) s->in_off[i + 1] += s->in_off[i];
+        memset(s->fill, 0, sizeof(int) * P);
+        for (int q = 0; q < P; ++q) /* ascending source order */
+            for (int k = 0; k < 3; ++k) {
+                const int r = s->links[3 * q + k];
+                s->in_src[s->in_off[r] + s->fill[r]++] = q;
+            }
+        s->topo = g;
+    }
+    for (int i = 0; i < P; ++i) { /* serial velocity loop, :807-845 */
+        /* informant = first argmin of pcost over find(L.col(i)==1) (:810-812):
+         * candidates are {i} U incoming, lowest index wins ties */
+        int inf = -1;
+        double best = 0;
+        int lo = s->in_off[i], hi = s->in_off[i + 1], e = lo;
+        int self_done = 0;
+        for (;;) { /* merge self into the ascending incoming list */
+            int q;
+            if (!self_done && (e >= hi || i <= s->in_src[e])) {
+                q = i;
+                self_done = 1;
+            } else if (e < hi) {
+                q = s->in_src[e++];
+            } else
+                break;
+            if (inf < 0 || s->pc[q] < best) {
+                best = s->pc[q];
+                inf = q;
+            }
+        }
+        double *xi = s->x + D * i, *vi = s->v + D * i;
+        const double *pbi = s->pb + D * i, *pbn = s->pb + D * inf;
+        int self_inf = (inf == i);
+        if (ext) { /* the exchanged candidate wins strictly (NaN costs as +inf) */
+            const double bc = (best != best) ? INFINITY : best;
+            if (ext[D] < bc) {
+                pbn = ext;
+                self_inf = 0;
+            }
+        }
+        for (int d = 0; d < D; ++d) {
+            const double rp = ora_u01(seed, ST_RP, (uint32_t)g, (uint32_t)i, (uint32_t)d);
+            const double rg = ora_u01(seed, ST_RG, (uint32_t)g, (uint32_t)i, (uint32_t)d);
+            if (self_inf)
+                vi[d] = W1 * vi[d] + (C1 * rp) * (pbi[d] - xi[d]);
+            else
+                vi[d] = (W1 * vi[d] + (C1 * rp) * (pbi[d] - xi[d])) +
+                        (C2 * rg) * (pbn[d] - xi[d]);
+        }
+        for (int d = 0; d < D; ++d) xi[d] = xi[d] + vi[d];
+        check_constraints(xi, vi, lb, ub);
+    }
+    ora_eval_costs(h, o, s->x, P, 0, s->fx, nthreads); /* :848-861 */
+    for (int i = 0; i < P; ++i)
+        if (s->fx[i] < s->pc[i]) {
+            s->pc[i] = s->fx[i];
+            memcpy(s->pb + D * i, s->x + D * i, sizeof(double) * D);
+        }
+    const int fid = arma_argmin(s->pc, P); /* pcost.min(fmin_id), :864-865 */
+    const double fmin = s->pc[fid];
+    if (fmin < s->gcost) { /* gbest = particles.col(fmin_id), :869-873 */
+        memcpy(s->gpos, s->x + D * fid, sizeof(s->gpos));
+        s->gcost = fmin;
+        s->count = 0;
+    } else
+        s->count += 1;
+    if (trace) {
+        if (trace->gbest_trace) trace->gbest_trace[g - 1] = s->gcost;
+        if (trace->fmin_trace) trace->fmin_trace[g - 1] = fmin;
+        if (trace->count_trace) trace->count_trace[g - 1] = s->count;
+        if (trace->topo_trace) trace->topo_trace[g - 1] = s->topo;
+    }
+}
+
 int ora_pso_evolve(const ora_hand *h, const ora_obs *o, const double x0[26], int P,
                    int maxiter, const double lb[26], const double ub[26],
                    const double stdv[26], uint64_t seed, double bestp[26],
                    double *bestcost, ora_pso_trace *trace, int nthreads) {
+    ora_swarm s;
+    swarm_init(&s, h, o, x0, P, stdv, seed, trace, nthreads);
+    for (int g = 1; g < maxiter; ++g) swarm_gen(&s, h, o, g, lb, ub, NULL, trace, nthreads);
+    memcpy(bestp, s.gpos, sizeof(s.gpos));
+    if (bestcost) *bestcost = s.gcost;
+    swarm_free(&s);
+    return 1;
+}
+
+/* The opt-in per-generation exchange of R subswarms (hpe_set_exchange; TEST
+ * INFRASTRUCTURE mirror of a non-reference extension): swarm r runs with seeds[r]; after
+ * every `every`-th generation g < maxiter - 1 each swarm's best pbest {pb row, pc} (first
+ * argmin, NaN as +inf) is formed, the best over swarms (lowest cost, ties to the lowest r;
+ * NaN never wins) becomes every swarm's extra informant candidate for the following
+ * generations.  bestp: R x 26, bestcost: R. */
+int ora_pso_evolve_xch(const ora_hand *h, const ora_obs *o, const double x0[26], int P,
+                       int maxiter, const double lb[26], const double ub[26],
+                       const double stdv[26], const uint64_t *seeds, int R, int every,
+                       double *bestp, double *bestcost, int nthreads) {
     const int D = ORA_DOF;
-    double *x = (double *)calloc((size_t)D * P, sizeof(double));
-    double *v = (double *)calloc((size_t)D * P, sizeof(double));
-    double *pb = (double *)calloc((size_t)D * P, sizeof(double));
-    double *pc = (double *)calloc((size_t)P, sizeof(double));
-    double *fx = (double *)calloc((size_t)P, sizeof(double));
-    int *links = (int *)calloc((size_t)3 * P, sizeof(int));
-    int *in_off = (int *)calloc((size_t)P + 1, sizeof(int));
-    int *in_src = (int *)calloc((size_t)3 * P, sizeof(int));
-    int *fill = (int *)calloc((size_t)P, sizeof(int));
-    double gpos[26], gcost = 1e100;
-    memset(gpos, 0, sizeof(gpos));
-
-    /* generate_particles, PSO.cpp:56-74 */
-    ora_normals(seed, P, x);
-    for (int i = 0; i < P; ++i)
-        for (int d = 0; d < D; ++d) x[D * i + d] = x0[d] + x[D * i + d] * stdv[d];
-    memcpy(pb, x, sizeof(double) * D * P);
-    ora_eval_costs(h, o, x, P, 0, pc, nthreads); /* PSO.cpp:748-763 */
-    if (trace && trace->pcost0) memcpy(trace->pcost0, pc, sizeof(double) * P);
-    for (int i = 0; i < P; ++i) /* serial semantics of the racy init update */
-        if (pc[i] < gcost) {
-            gcost = pc[i];
-            memcpy(gpos, x + D * i, sizeof(gpos));
-        }
-
-    const double W1 = 1. / (2 * log(2.0)), C1 = 0.5 + log(2.0), C2 = C1; /* :772-774 */
-    int count = 100, topo = -1;
-    for (int g = 1; g < maxiter; ++g) { /* iter 2..maxiter, :778-780 */
-        if (count > 0) { /* topology rebuild, :790-803 */
-            for (int s = 0; s < P; ++s)
-                for (int k = 0; k < 3; ++k) {
-                    const double u = ora_u01(seed, ST_LINK, (uint32_t)g, (uint32_t)s, (uint32_t)k);
-                    links[3 * s + k] = (int)floor(u * (P - 1) + 0.5);
+    ora_swarm *s = (ora_swarm *)calloc((size_t)R, sizeof(ora_swarm));
+    for (int r = 0; r < R; ++r) swarm_init(&s[r], h, o, x0, P, stdv, seeds[r], NULL, nthreads);
+    double ext[27];
+    int have_ext = 0;
+    for (int g = 1; g < maxiter; ++g) {
+        for (int r = 0; r < R; ++r)
+            swarm_gen(&s[r], h, o, g, lb, ub, have_ext ? ext : NULL, NULL, nthreads);
+        if (every > 0 && g % every == 0 && g < maxiter - 1) {
+            double bc = INFINITY;
+            int br = 0, bi = 0;
+            for (int r = 0; r < R; ++r) {
+                int id = 0;
+                double m = INFINITY;
+                for (int i = 0; i < P; ++i) {
+                    const double v = s[r].pc[i] != s[r].pc[i] ? INFINITY : s[r].pc[i];
+                    if (v < m) {
+                        m = v;
+                        id = i;
+                    }
                 }
-            memset(in_off, 0, sizeof(int) * (P + 1));
-            for (int e = 0; e < 3 * P; ++e) in_off[links[e] + 1]++;
-            for (int i = 0; i < P; ++i) in_off[i + 1] += in_off[i];
-            memset(fill, 0, sizeof(int) * P);
-            for (int s = 0; s < P; ++s) /* ascending source order */
-                for (int k = 0; k < 3; ++k) {
-                    const int r = links[3 * s + k];
-                    in_src[in_off[r] + fill[r]++] = s;
-                }
-            topo = g;
-        }
-        for (int i = 0; i < P; ++i) { /* serial velocity loop, :807-845 */
-            /* informant = first argmin of pcost over find(L.col(i)==1) (:810-812):
-             * candidates are {i} U incoming, lowest index wins ties */
-            int inf = -1;
-            double best = 0;
-            int lo = in_off[i], hi = in_off[i + 1], e = lo;
-            int self_done = 0;
-            for (;;) { /* merge self into the ascending incoming list */
-                int s;
-                if (!self_done && (e >= hi || i <= in_src[e])) {
-                    s = i;
-                    self_done = 1;
-                } else if (e < hi) {
-                    s = in_src[e++];
-                } else
-                    break;
-                if (inf < 0 || pc[s] < best) {
-                    best = pc[s];
-                    inf = s;
+                if (r == 0 || m < bc) {
+                    bc = m;
+                    br = r;
+                    bi = id;
                 }
             }
-            double *xi = x + D * i, *vi = v + D * i;
-            const double *pbi = pb + D * i, *pbn = pb + D * inf;
-            for (int d = 0; d < D; ++d) {
-                const double rp = ora_u01(seed, ST_RP, (uint32_t)g, (uint32_t)i, (uint32_t)d);
-                const double rg = ora_u01(seed, ST_RG, (uint32_t)g, (uint32_t)i, (uint32_t)d);
-                if (inf == i)
-                    vi[d] = W1 * vi[d] + (C1 * rp) * (pbi[d] - xi[d]);
-                else
-                    vi[d] = (W1 * vi[d] + (C1 * rp) * (pbi[d] - xi[d])) +
-                            (C2 * rg) * (pbn[d] - xi[d]);
-            }
-            for (int d = 0; d < D; ++d) xi[d] = xi[d] + vi[d];
-            check_constraints(xi, vi, lb, ub);
-        }
-        ora_eval_costs(h, o, x, P, 0, fx, nthreads); /* :848-861 */
-        for (int i = 0; i < P; ++i)
-            if (fx[i] < pc[i]) {
-                pc[i] = fx[i];
-                memcpy(pb + D * i, x + D * i, sizeof(double) * D);
-            }
-        const int fid = arma_argmin(pc, P); /* pcost.min(fmin_id), :864-865 */
-        const double fmin = pc[fid];
-        if (fmin < gcost) { /* gbest = particles.col(fmin_id), :869-873 */
-            memcpy(gpos, x + D * fid, sizeof(gpos));
-            gcost = fmin;
-            count = 0;
-        } else
-            count += 1;
-        if (trace) {
-            if (trace->gbest_trace) trace->gbest_trace[g - 1] = gcost;
-            if (trace->fmin_trace) trace->fmin_trace[g - 1] = fmin;
-            if (trace->count_trace) trace->count_trace[g - 1] = count;
-            if (trace->topo_trace) trace->topo_trace[g - 1] = topo;
+            memcpy(ext, s[br].pb + D * bi, sizeof(double) * D);
+            ext[D] = s[br].pc[bi];
+            have_ext = 1;
         }
     }
-    memcpy(bestp, gpos, sizeof(gpos));
-    if (bestcost) *bestcost = gcost;
-    free(x); free(v); free(pb); free(pc); free(fx);
-    free(links); free(in_off); free(in_src); free(fill);
+    for (int r = 0; r < R; ++r) {
+        memcpy(bestp + D * r, s[r].gpos, sizeof(s[r].gpos));
+        if (bestcost) bestcost[r] = s[r].gcost;
+        swarm_free(&s[r]);
+    }
+    free(s);
     return 1;
 }
 

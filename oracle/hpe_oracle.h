@@ -87,6 +87,13 @@ int ora_pso_evolve(const ora_hand *h, const ora_obs *o, const double x0[26], int
                    const double stdv[26], uint64_t seed, double bestp[26],
                    double *bestcost, ora_pso_trace *trace, int nthreads);
 
+/* the opt-in per-generation exchange of R subswarms (hpe_set_exchange), TEST mirror of a
+ * non-reference extension: bestp R x 26, bestcost R */
+int ora_pso_evolve_xch(const ora_hand *h, const ora_obs *o, const double x0[26], int P,
+                       int maxiter, const double lb[26], const double ub[26],
+                       const double stdv[26], const uint64_t *seeds, int R, int every,
+                       double *bestp, double *bestcost, int nthreads);
+
 int ora_refine_init_pose(const ora_hand *h, const ora_obs *o, double x0[26]);
 /* The same with test instrumentation: rigid != 0 runs the mirror of the GPU's hand-frame
  * refine (NOT the reference's operation order; hpe_oracle.c); margins[0..cap) receives

@@ -88,6 +88,10 @@ class Oracle:
         L.ora_refine_init_pose.argtypes = [C.POINTER(OraHand), C.POINTER(OraObs), dp]
         L.ora_refine_init_pose.restype = C.c_int
         L.ora_refine_last_margin.restype = C.c_double
+        L.ora_pso_evolve_xch.argtypes = [C.POINTER(OraHand), C.POINTER(OraObs), dp, C.c_int,
+                                         C.c_int, dp, dp, dp, C.POINTER(C.c_uint64), C.c_int,
+                                         C.c_int, dp, dp, C.c_int]
+        L.ora_pso_evolve_xch.restype = C.c_int
         L.ora_refine_ex.argtypes = [C.POINTER(OraHand), C.POINTER(OraObs), dp, C.c_int,
                                     C.POINTER(C.c_int), C.c_int, dp, C.c_int,
                                     C.POINTER(C.c_int)]
@@ -180,6 +184,21 @@ class Oracle:
         n = maxiter - 1
         return bp, bc.value, dict(gbest=tg[:n], fmin=tf[:n], count=tc[:n], topo=tt[:n],
                                   pcost0=p0)
+
+    def pso_evolve_xch(self, h, obs, x0, P, maxiter, lb, ub, sd, seeds, every, nthreads=0):
+        """R subswarms (seeds) with the opt-in per-generation exchange every `every`
+        generations (hpe_set_exchange's mirror; every = 0: independent swarms).  Returns
+        (bestp R x 26, bestcost R)."""
+        x = np.ascontiguousarray(x0, dtype=np.float64)
+        lb, ub, sd = (np.ascontiguousarray(a, dtype=np.float64) for a in (lb, ub, sd))
+        sa = np.ascontiguousarray(seeds, dtype=np.uint64)
+        R = len(sa)
+        bp = np.zeros((R, 26)); bc = np.zeros(R)
+        self.lib.ora_pso_evolve_xch(C.byref(h), C.byref(obs.s), _p(x, C.c_double), P, maxiter,
+                                    _p(lb, C.c_double), _p(ub, C.c_double), _p(sd, C.c_double),
+                                    _p(sa, C.c_uint64), R, every, _p(bp, C.c_double),
+                                    _p(bc, C.c_double), nthreads)
+        return bp, bc
 
     def pso_optimise(self, h, obs, x0, P, maxiter, lb, ub, sd, w, c1, c2, seed=1000,
                      nthreads=0):

@@ -21,19 +21,23 @@ import oracle_np
 pytestmark = pytest.mark.gpu
 
 
-def test_bench_two_ranks_same_device_gloo(tmp_path, oracle, ora_hand):
+def _bench_ranks(dump, *extra):
     env = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
-    dump = tmp_path / "dump"
     cmd = [sys.executable, str(hand_data.ROOT / "bench.py"), "--gpus", "2", "--backend", "gloo",
            "--same-device", "--config", "subswarm8", "--steps", "3", "--warmup", "1",
-           "--no-cpu-baseline", "--dump", str(dump)]
+           "--no-cpu-baseline", "--dump", str(dump), *extra]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, out.stdout
-    r = json.loads(lines[0])
+    return json.loads(lines[0])
+
+
+def test_bench_two_ranks_same_device_gloo(tmp_path, oracle, ora_hand):
+    dump = tmp_path / "dump"
+    r = _bench_ranks(dump)
     assert r["n_gpus"] == 2 and r["config"]["particles"] == 1024 and r["value"] > 0
     # the multi-rank self-verification the 8-GPU run will carry (bench.py rank_report)
     rk = r["ranks"]
@@ -58,3 +62,25 @@ def test_bench_two_ranks_same_device_gloo(tmp_path, oracle, ora_hand):
     cbest, _, xbest = min(res, key=lambda e: (e[0], e[1]))
     np.testing.assert_allclose(st[0][0, :26], xbest, rtol=0, atol=1e-6)
     assert abs(st[0][0, 26] - cbest) <= 1e-8 * abs(cbest)
+
+
+def test_bench_two_ranks_generation_exchange(tmp_path, oracle, ora_hand):
+    """The opt-in ICP-PSO style exchange (--exchange gen:10, hpe_set_exchange; NOT the
+    reference algorithm): every 10 generations the two ranks' best pbest is all-gathered
+    and the best injected as an extra informant.  Frame 0 against the oracle's lockstep
+    mirror of the two subswarms (ora_pso_evolve_xch), then the per-frame best-of-2."""
+    dump = tmp_path / "dump"
+    r = _bench_ranks(dump, "--exchange", "gen:10")
+    assert "every 10 generations" in r["config"]["exchange"]
+    st = [np.load(dump / f"states_rank{k}.npy") for k in range(2)]
+    np.testing.assert_array_equal(st[0], st[1])
+    raw0, x0 = np.load(dump / "raw0.npy"), np.load(dump / "x0.npy")
+    obs = oracle.preprocess(raw0)
+    ub, lb, sd = oracle_np.reference_bounds()
+    xr, _ = oracle.refine(ora_hand, obs, x0, rigid=REFINE_RIGID)
+    bp, bc = oracle.pso_evolve_xch(ora_hand, obs, xr, 1024, 31, lb, ub, sd, [1000, 1001], 10)
+    ind, _ = oracle.pso_evolve_xch(ora_hand, obs, xr, 1024, 31, lb, ub, sd, [1000, 1001], 0)
+    assert not np.array_equal(bp, ind)  # the exchange changed the swarms
+    k = int(np.argmin(bc))
+    np.testing.assert_allclose(st[0][0, :26], bp[k], rtol=0, atol=1e-6)
+    assert abs(st[0][0, 26] - bc[k]) <= 1e-8 * abs(bc[k])
