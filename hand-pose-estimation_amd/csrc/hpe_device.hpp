@@ -1165,6 +1165,103 @@ __device__ __forceinline__ FrozenHead frozen_head(FkSm &f, const DevObs &o,
            ((l < 16) ? collide_value(cp[2], rt[2]) : 0.0);
     return r;
 }
+// A whole Goldstein node of the rigid refine on one wave, for clouds of at most FP_MAX
+// points (the lane's matchIds in fp): the rotation rows are formed once, then the lane's own
+// sphere (stored for the accepted-node copy, projected for the depth term) and its four
+// points' matched centres are placed straight from the hand frame in registers -- the
+// same operations as rigid_wave, so the same bits -- with no LDS round trip between the
+// placement and the alignment.  All hand-frame / point reads are issued before the trig.
+// Returns cal_cost2(theta, matchId, false) = sum(align * lambda + depth) + R.C.
+template <int MODE, bool OUTLINE_TRIG = HPE_RIGID_OUTLINE_TRIG, class CV>
+__device__ __forceinline__ double rigid_node(FkSm &f, const DevObs &o, const CV &cv,
+                                             const DevHand *__restrict__ H, const RigidSm &R,
+                                             double thl, const FrozenPts &fp) {
+    const int l = threadIdx.x & 63;
+    const int sl = l < HPE_NS ? l : HPE_NS - 1;
+    const bool tr = MODE == RG_TRANS;
+    const double a0 = tr ? R.P[sl][0] : R.q[sl][0];
+    const double a1 = tr ? R.P[sl][1] : R.q[sl][1];
+    const double a2 = tr ? R.P[sl][2] : R.q[sl][2];
+    const double rr = H->radii[sl];
+    double px[4], py[4], pz[4], bx[4], by[4], bz[4], sr[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int q = min(l + 64 * k, cv.n - 1), id = fp.id[k];
+        px[k] = cv.cx[q];
+        py[k] = cv.cy[q];
+        pz[k] = cv.cz[q];
+        bx[k] = tr ? R.P[id][0] : R.q[id][0];
+        by[k] = tr ? R.P[id][1] : R.q[id][1];
+        bz[k] = tr ? R.P[id][2] : R.q[id][2];
+        sr[k] = H->radii[id];
+    }
+    const double u0 = readlane_f64(thl, 3), u1 = readlane_f64(thl, 4), u2 = readlane_f64(thl, 5);
+    double g[9];
+    if (!tr) {
+        double s = 0.0, c = 1.0;
+        if (l < 3) {  // TWS, ANG, ROT (fingermodel.cpp:91-93)
+            const double a = deg2rad(l == 0 ? thl + 180 : thl);
+            if (OUTLINE_TRIG) {
+                const SinCos r = sincos_outline(a);
+                s = r.s;
+                c = r.c;
+            } else {
+                sincos(a, &s, &c);
+            }
+        }
+        const double sz = readlane_f64(s, 0), cz = readlane_f64(c, 0);
+        const double sy = readlane_f64(s, 1), cy = readlane_f64(c, 1);
+        const double sx = readlane_f64(s, 2), cx = readlane_f64(c, 2);
+#pragma unroll
+        for (int r = 0; r < 3; ++r) rigid_row(r, sz, cz, sy, cy, sx, cx, g[3 * r], g[3 * r + 1], g[3 * r + 2]);
+    }
+    // coordinate r of a centre from its hand-frame (or, translation block, rotated) row
+    auto place = [&](double b0, double b1, double b2, int r, double u) {
+        const double p = tr ? (r == 0 ? b0 : r == 1 ? b1 : b2)
+                            : (g[3 * r] * b0 + g[3 * r + 1] * b1) + g[3 * r + 2] * b2;
+        return p + u;
+    };
+    // the lane's own sphere: stored (read after the round's barrier if this node is
+    // accepted) and projected
+    const double v0 = place(a0, a1, a2, 0, u0);
+    const double v1 = place(a0, a1, a2, 1, u1) * -1;  // handmodel.cpp:288
+    const double v2 = place(a0, a1, a2, 2, u2) * -1;
+    if (l < HPE_NS) {
+        f.S[l][0] = v0;
+        f.S[l][1] = v1;
+        f.S[l][2] = v2;
+        f.Sp[0][l] = (float)v0;
+        f.Sp[1][l] = (float)v1;
+        f.Sp[2][l] = (float)v2;
+    }
+    DepthG dg = depth_issue_at(SphXYZ{v0, v1, v2}, l, o, H);
+    dg.r = rr;
+    // the frozen alignment (align_frozen_pts' per-point operations)
+    double d2[4], rt[4], e[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const double sx0 = place(bx[k], by[k], bz[k], 0, u0);
+        const double sy0 = place(bx[k], by[k], bz[k], 1, u1) * -1;
+        const double sz0 = place(bx[k], by[k], bz[k], 2, u2) * -1;
+        const double dx = px[k] - sx0, dy = py[k] - sy0, dz = pz[k] - sz0;
+        d2[k] = (dx * dx + dy * dy) + dz * dz;
+        rt[k] = hpe_sqrt_nr(d2[k]);
+    }
+    if (!(hpe_sqrt_direct(d2[0]) && hpe_sqrt_direct(d2[1]) && hpe_sqrt_direct(d2[2]) &&
+          hpe_sqrt_direct(d2[3]))) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) rt[k] = hpe_sqrt_direct(d2[k]) ? rt[k] : sqrt(d2[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const double r = rt[k] - sr[k];
+        e[k] = (l + 64 * k < cv.n) ? r * r : 0.0;
+    }
+    const double al = (e[0] + e[1]) + (e[2] + e[3]);
+    const double dep = depth_finish(dg, o, l < HPE_NS);
+    return wave_sum((al * o.lambda + dep) + 0.0) + R.C;
+}
+
 // frozen_head of the rigid refine (rigid_wave above): the collision is the constant R.C,
 // added by the caller after the sum.
 template <int MODE>

@@ -215,36 +215,87 @@ __device__ __forceinline__ void push_inbox(const DevSwarm &sw, int g, int s, int
     push_inbox(sw, g, s, q, L.ok ? (int)(L.raw & 0xffffffff) : -1, (int)(L.raw >> 32), tt, pc, row);
 }
 
-__global__ __launch_bounds__(HPE_NT) void k_pso_init(DevSwarm sw, const double *__restrict__ x0,
-                                                     const DevObs *__restrict__ og, const DevHand *__restrict__ Hg) {
+// The split forms (SPLIT > 1, large clouds): block `slice` of particle i has summed its
+// slice of the cost into fx; its partial goes to sw.part and the last of the particle's
+// SPLIT blocks to arrive adds them in slice order (deterministic) into fx and returns
+// true; the others return false and are done.  Release: the partial stored, agent fence,
+// counter; acquire: one lane, then the barrier.
+template <int SPLIT>
+__device__ __forceinline__ bool split_arrive(const DevSwarm &sw, int g, int i, int slice,
+                                             double &fx, Smem &sm) {
+    __shared__ int last_blk;
+    if (threadIdx.x == 0) {
+        double *pp = sw.part + ((size_t)(g & 1) * sw.P + i) * SPLIT;
+        unsigned *ctr = sw.arrive + (size_t)(g & 1) * sw.P + i;
+        pp[slice] = fx;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const unsigned prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool last = prev == SPLIT - 1;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            double tot = 0.0;
+#pragma unroll
+            for (int k = 0; k < SPLIT; ++k) tot += pp[k];
+            *ctr = 0u;  // next used two generations on, after kernel boundaries
+            sm.dscal[6] = tot;
+        }
+        last_blk = last ? 1 : 0;
+    }
+    __syncthreads();
+    if (!last_blk) return false;
+    fx = sm.dscal[6];
+    return true;
+}
+
+// generate_particles + the initial evaluation (PSO.cpp:56-74, 748-763).  SPLIT > 1: the
+// split form of k_pso_gen_split (the same slices and sums, so a particle's cost of the same
+// theta is the same bits in both kernels).
+template <int NT, int SPLIT>
+__device__ __forceinline__ void pso_init_body(const DevSwarm &sw, const double *__restrict__ x0,
+                                              const DevObs *__restrict__ og,
+                                              const DevHand *__restrict__ Hg) {
     const DevObs o = *og;  // the selected frame (device-resident: graph-stable args)
     __shared__ Smem sm;
-    const int i = blockIdx.x, t = threadIdx.x;
-    const double hw = hand_word<HPE_NT>(Hg);
+    const int P = sw.P, t = threadIdx.x;
+    const int i = SPLIT == 1 ? (int)blockIdx.x : (int)blockIdx.x % P;
+    const int slice = SPLIT == 1 ? 0 : (int)blockIdx.x / P;
+    const double hw = hand_word<NT>(Hg);
     const DevHand *__restrict__ H = &sm.hand;
     const double *sd = sw.bounds + 2 * HPE_DOF;
     // pushing lanes: waves 1..3 (q = t - 64), topology 1 = rebuilt for gen 1
     const int q = t - 64;
     const Link lk = load_link(sw, 0, i, q, 1, q < 3 * IB_FIELDS);
-    const CloudGlobal cv = obs_cloud(o);
+    CloudGlobal cv = obs_cloud(o);
+    if (SPLIT > 1) {  // this block's slice of the cloud (as k_pso_gen_split)
+        const int per = (o.n + SPLIT - 1) / SPLIT, s0 = min(slice * per, o.n);
+        cv = CloudGlobal{cv.cx + s0, cv.cy + s0, cv.cz + s0, min(s0 + per, o.n) - s0};
+    }
     const Pt pre = load_pt(cv, t);
     if (t < HPE_DOF) {  // particles = x0 + randn % std (PSO.cpp:67-72)
         const size_t e = (size_t)i * HPE_DOF + t;
         const double x = x0[t] + sw.normals[e] * sd[t];
         sm.fk.th[t] = x;
-        sw.xh[e] = x;
-        sw.pb[e] = x;
-        sw.v[e] = 0.0;
+        if (slice == 0) {
+            sw.xh[e] = x;
+            sw.pb[e] = x;
+            sw.v[e] = 0.0;
+        }
     }
-    if (sw.ext && i == 0 && t == 0) sw.ext[HPE_DOF] = __builtin_inf();  // no candidate yet
-    hand_put<HPE_NT>(sm.hand, hw);
+    if (sw.ext && i == 0 && slice == 0 && t == 0) sw.ext[HPE_DOF] = __builtin_inf();  // no candidate yet
+    hand_put<NT>(sm.hand, hw);
     __syncthreads();
-    const double c = eval_block<EV_COST, HPE_NT>(sm, o, cv, H, nullptr, pre);
+    double c = eval_block<EV_COST, NT>(sm, o, cv, H, nullptr, pre, BT_GENS, nullptr, slice == 0);
+    if (SPLIT > 1 && !split_arrive<SPLIT>(sw, 0, i, slice, c, sm)) return;
     if (t == 0) {  // PSO.cpp:748-763; pbest costs are >= 0, so their bits order like values
         sw.pch[i] = c;
         gmin_lower(sw, 0, i, c);
     }
     push_inbox(sw, 0, i, q, lk, 1, c, sm.fk.th);
+}
+
+__global__ __launch_bounds__(HPE_NT) void k_pso_init(DevSwarm sw, const double *__restrict__ x0,
+                                                     const DevObs *__restrict__ og, const DevHand *__restrict__ Hg) {
+    pso_init_body<HPE_NT, 1>(sw, x0, og, Hg);
 }
 
 // One fused generation g >= 1 (PSO.cpp:781-879).  Wave 0 carries the serial part: every
@@ -446,32 +497,7 @@ __device__ __forceinline__ void pso_gen_body(const DevSwarm &sw, const DevObs *_
     // ---- evaluation and pbest (PSO.cpp:848-861)
     double fx = eval_block<EV_COST, NT, false>(sm, o, cv, H, nullptr, pre, g, &own0, slice == 0);
     BLK_TS(g, 4);
-    if (SPLIT > 1) {
-        // slice totals in sw.part; the last block of the particle to arrive adds them in
-        // slice order (deterministic) and carries on; the others are done.  Release: the
-        // partial drained, agent fence, counter; acquire: one lane, then the barrier.
-        __shared__ int last_blk;
-        if (t == 0) {
-            double *pp = sw.part + ((size_t)(g & 1) * P + i) * SPLIT;
-            unsigned *ctr = sw.arrive + (size_t)(g & 1) * P + i;
-            pp[slice] = fx;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            const unsigned prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const bool last = prev == SPLIT - 1;
-            if (last) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                double tot = 0.0;
-#pragma unroll
-                for (int k = 0; k < SPLIT; ++k) tot += pp[k];
-                *ctr = 0u;  // next used two generations on, after kernel boundaries
-                sm.dscal[6] = tot;
-            }
-            last_blk = last ? 1 : 0;
-        }
-        __syncthreads();
-        if (!last_blk) return;
-        fx = sm.dscal[6];
-    }
+    if (SPLIT > 1 && !split_arrive<SPLIT>(sw, g, i, slice, fx, sm)) return;
     sc.start();
     const bool better = fx < pci;
     const double pn = better ? fx : pci;
@@ -501,6 +527,13 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
 // threads per particle, three resident per CU (<= 168 VGPRs).
 #define PSO_SPLIT 3
 #define PSO_SPLIT_NT 256
+template <int SPLIT>
+__global__ __launch_bounds__(PSO_SPLIT_NT, 3) void k_pso_init_split(DevSwarm sw,
+                                                                   const double *__restrict__ x0,
+                                                                   const DevObs *__restrict__ og,
+                                                                   const DevHand *__restrict__ Hg) {
+    pso_init_body<PSO_SPLIT_NT, SPLIT>(sw, x0, og, Hg);
+}
 template <int SPLIT>
 __global__ __launch_bounds__(PSO_SPLIT_NT, 3) void k_pso_gen_split(DevSwarm sw,
                                                                   const DevObs *__restrict__ og,
@@ -788,8 +821,20 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
                                                       unsigned long long *__restrict__ seq_dev = nullptr,
                                                       unsigned long long *done_host = nullptr,
                                                       double *__restrict__ hist = nullptr,
-                                                      const int *__restrict__ fail = nullptr) {
+                                                      const int *__restrict__ fail = nullptr,
+                                                      const DevObs *__restrict__ seq_table = nullptr,
+                                                      DevObs *__restrict__ seq_obs = nullptr,
+                                                      int *__restrict__ seq_cur = nullptr) {
     constexpr int CH = 2048;  // generations staged per pass
+    // offline sequences (hpe_track_sequence_dev): the frame's history row and slot come
+    // from the device cursor {slot, row}, and the next frame's descriptor is staged into the
+    // descriptor every kernel of the chunk graph reads -- the graph is independent of the
+    // slot range it tracks
+    int seq_slot = 0;
+    if (TAIL && seq_cur) {
+        seq_slot = seq_cur[0];
+        if (hist) hist += (size_t)(HPE_DOF + 1) * seq_cur[1];
+    }
     // a timed-out multi-workgroup refine (DevMw::err, set until the host has reported it):
     // this frame's result is undefined, so bestp and cost become NaN
     const int failed = (TAIL && fail) ? __hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
@@ -948,6 +993,17 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
     for (int c = t; c < (G + 1) * GMIN_SHARDS; c += HPE_NT) sw.gmin[(size_t)c * GMIN_STRIDE] = ~0ull;
     if (TAIL) {
         if (obs_out && t < (int)(sizeof(DevObs) / 8)) ((unsigned long long *)obs_out)[t] = obs_word;
+        if (seq_cur) {
+            // the next frame's descriptor for the next frame's kernels (stream order: they
+            // start after this kernel); the slot after the last is never read
+            const int nx = seq_slot + 1 < HPE_MAX_SLOTS ? seq_slot + 1 : seq_slot;
+            if (t < (int)(sizeof(DevObs) / 8))
+                ((unsigned long long *)seq_obs)[t] = ((const unsigned long long *)(seq_table + nx))[t];
+            if (t == 0) {
+                seq_cur[0] = seq_slot + 1;
+                seq_cur[1] = seq_cur[1] + 1;
+            }
+        }
         if (failed) {
             if (t <= HPE_DOF) {
                 out[t] = __builtin_nan("");
@@ -966,6 +1022,19 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
             out[HPE_DOF] = c;
             if (hist) hist[HPE_DOF] = c;
         }
+    }
+}
+
+// Start of an offline sequence (hpe_track_sequence_dev): the first frame's descriptor into
+// the chunk graphs' descriptor, the cursor to {first slot, history row 0}.
+__global__ void k_seq_begin(const DevObs *__restrict__ table, int first, DevObs *__restrict__ cur_obs,
+                            int *__restrict__ cur) {
+    const int t = threadIdx.x;
+    if (t < (int)(sizeof(DevObs) / 8))
+        ((unsigned long long *)cur_obs)[t] = ((const unsigned long long *)(table + first))[t];
+    if (t == 0) {
+        cur[0] = first;
+        cur[1] = 0;
     }
 }
 
@@ -1147,7 +1216,10 @@ __device__ __forceinline__ void eval_nodes(RefineSm &rs, int nn, const DevObs &o
         if (w < nn) {
             wave_sync();
             double f;
-            if (RIGID) {
+            if (RIGID && fp) {  // small clouds: the fused node (no LDS round trip inside)
+                f = rblk ? rigid_node<RG_TRANS>(rs.w[w], o, cv, H, rs.rg, *thr, *fp)
+                         : rigid_node<RG_ROT>(rs.w[w], o, cv, H, rs.rg, *thr, *fp);
+            } else if (RIGID) {
                 const FrozenHead hd = rblk ? rigid_head<RG_TRANS>(rs.w[w], o, H, rs.rg, *thr)
                                            : rigid_head<RG_ROT>(rs.w[w], o, H, rs.rg, *thr);
                 f = frozen_tail(rs.w[w], o, cv, H, match, hd, fp) + rs.rg.C;

@@ -64,6 +64,7 @@ SIGNATURES = {
     "hpe_pso_trace": (C.c_int, [C.c_void_p, dp, ip, ip, C.c_int]),
     "hpe_refine_init_pose": (C.c_int, [C.c_void_p, dp, ip]),
     "hpe_set_refine_exact": (C.c_int, [C.c_void_p, C.c_int]),
+    "hpe_graph_captures": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
     "hpe_set_exchange": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]),
     "hpe_get_refine_exact": (C.c_int, [C.c_void_p]),
     "hpe_track_frame": (C.c_int, [C.c_void_p, C.c_int, C.c_int, dp, dp]),

@@ -206,7 +206,10 @@ int hpe_track_frame_dev(hpe_ctx *ctx, int num_p, int refine, double *d_state);
  * hpe_prepare_frame), each tracked exactly like hpe_track_frame_dev on its own slot and
  * d_state carried from frame to frame.  Frames are captured frames_per_graph at a time
  * into one graph (0: HPE_SEQ_CHUNK), so the graph-to-graph gap is paid once per chunk;
- * captured chunks are cached per slot range.  d_hist (device, optional): n x 27 doubles,
+ * the chunk graphs read each frame's descriptor and history row through a device cursor
+ * (k_seq_begin starts it, each frame's final kernel advances it), so a captured chunk
+ * serves every chunk of the same shape (frames, kernel forms, d_state, d_hist) wherever
+ * its slots lie.  d_hist (device, optional): n x 27 doubles,
  * frame f's {bestp, cost}.  Asynchronous on hpe_stream(ctx); the last frame is the
  * selected one afterwards, and a later hpe_prepare_frame waits for the sequence. */
 #define HPE_SEQ_CHUNK 8
@@ -251,6 +254,10 @@ int hpe_profile_read_kernel(hpe_ctx *ctx, int kernel, int32_t *launches, double 
  * the context was created or last reset (bench instrumentation: the algorithmic work of
  * the k_refine launches).  Synchronises; reset != 0 zeroes the count after reading. */
 int hpe_refine_eval_count(hpe_ctx *ctx, uint64_t *total, int reset);
+
+/* Number of graphs this context has captured (tracking graphs are captured once per shape
+ * and replayed; tests check that a replay captured nothing). */
+int hpe_graph_captures(const hpe_ctx *ctx, uint64_t *n);
 
 /* Diagnostic build only (libhpe_stamps.so): per-phase shader-clock cycle sums
  * [0..31] and lap counts [32..63] of block 0, reset on read.  Returns 1 in the

@@ -164,16 +164,27 @@ def test_sequence_tracking_like_oracle_and_per_frame(gh, oracle, ora_hand, np_ha
         cr = oracle.cal_cost(ora_hand, obs, x_ref)
         np.testing.assert_allclose(per_frame[f, :26], x_ref, rtol=0, atol=1e-6)
         assert abs(per_frame[f, 26] - cr) <= 1e-8 * abs(cr)
-    for K in (1, 3, 8, 3):  # the last: cached graphs
+    hist = torch.empty((n, 27), dtype=torch.float64, device="cuda:0")  # one buffer: a graph key
+    caps = C.c_uint64(0)
+    seen = set()  # chunk lengths captured so far: a chunk graph is keyed by its shape only
+    for it, K in enumerate((1, 3, 8, 3)):  # the last: cached graphs
         st[:26] = torch.from_numpy(oracle_np.X0)
         st[26] = 0.0
-        hist = torch.full((n, 27), float("nan"), dtype=torch.float64, device="cuda:0")
+        hist.fill_(float("nan"))
         torch.cuda.synchronize()
+        gh.ctx.check(rt.hpe_graph_captures(gh.ctx.h, C.byref(caps)))
+        before = caps.value
         gh.ctx.track_sequence(P, 1, st.data_ptr(), s0, n, K, hist.data_ptr())
         gh.ctx.check(rt.hpe_sync(gh.ctx.h))
+        gh.ctx.check(rt.hpe_graph_captures(gh.ctx.h, C.byref(caps)))
         h = hist.cpu().numpy()
         assert np.array_equal(h, per_frame), K
         assert np.array_equal(st.cpu().numpy(), per_frame[-1]), K
+        # chunk graphs are keyed by shape, not slots: 7 frames in chunks of K capture one
+        # graph per chunk length not seen before (none on the replay)
+        lens = {min(K, n - f0) for f0 in range(0, n, K)}
+        assert caps.value - before == len(lens - seen), (K, caps.value - before)
+        seen |= lens
     # argument errors
     bad = rt.hpe_track_sequence_dev
     assert bad(gh.ctx.h, P, 1, C.c_void_p(st.data_ptr()), s0, 0, 0, None) == hpe._lib.HPE_E_ARG
