@@ -177,7 +177,7 @@ __device__ __forceinline__ double gmin_read(const DevSwarm &sw, int g) {
 }
 
 __device__ __forceinline__ size_t ib_index(const DevSwarm &sw, int par, int var, int r, int slot) {
-    return ((((size_t)par * 2 + var) * sw.P + r) * sw.K + slot) * IB_FIELDS;
+    return ((((size_t)par * 2 + var) * sw.P + r) * sw.K + slot) * IB_STRIDE;
 }
 
 // Push {tag = (g, topology, s), pbest cost, pbest row} of particle s after generation g
@@ -285,7 +285,9 @@ __device__ __forceinline__ void pso_init_body(const DevSwarm &sw, const double *
     hand_put<NT>(sm.hand, hw);
     __syncthreads();
     double c = eval_block<EV_COST, NT>(sm, o, cv, H, nullptr, pre, BT_GENS, nullptr, slice == 0);
-    if (SPLIT > 1 && !split_arrive<SPLIT>(sw, 0, i, slice, c, sm)) return;
+    if constexpr (SPLIT > 1) {
+        if (!split_arrive<SPLIT>(sw, 0, i, slice, c, sm)) return;
+    }
     if (t == 0) {  // PSO.cpp:748-763; pbest costs are >= 0, so their bits order like values
         sw.pch[i] = c;
         gmin_lower(sw, 0, i, c);
@@ -310,7 +312,12 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_init(DevSwarm sw, const double *
 // sw.part, and the last of the SPLIT to arrive (agent-scope release / acquire counter)
 // sums the partials in slice order and does pbest, gmin and the pushes.  More resident
 // waves per SIMD for a search of ~10^4 points than one 512-thread workgroup gives.
-template <int NT, int SPLIT>
+// XCH: the opt-in per-generation exchange (sw.ext) is compiled in (k_pso_gen_x and the
+// XCH forms); the default kernels carry none of it.  ROW16: every inbox holds at most 15
+// slots (sw.K <= 15, the host's choice of instantiation): the informant argmin runs on one
+// 16-lane DPP row.  (A run-time K test left one body for both cases: the compiler no longer
+// duplicated the kernel per case, and the generation ran 0.15 us slower.)
+template <int NT, int SPLIT, bool XCH = false, bool ROW16 = true>
 __device__ __forceinline__ void pso_gen_body(const DevSwarm &sw, const DevObs *__restrict__ og,
                                              const DevHand *__restrict__ Hg, int g, double W1,
                                              double C1, double C2, const InboxCounts &kin) {
@@ -364,7 +371,7 @@ __device__ __forceinline__ void pso_gen_body(const DevSwarm &sw, const DevObs *_
         // ---- waves 1..7: both informant inboxes (payload rows) into LDS
         // the k0 valid kept slots, then the k1 valid rebuilt ones
         const double *src = sw.inbox + ib_index(sw, (g - 1) & 1, 0, i, 0);
-        const size_t var_stride = (size_t)P * K * IB_FIELDS;
+        const size_t var_stride = (size_t)P * K * IB_STRIDE;
         const int n = (k0 + k1) * IB_FIELDS, u0 = t - 64;
         constexpr int NL = (2 * IB_KMAX * IB_FIELDS + NT - 65) / (NT - 64);  // loads per lane
         double a[NL];
@@ -372,7 +379,9 @@ __device__ __forceinline__ void pso_gen_body(const DevSwarm &sw, const DevObs *_
         for (int k = 0; k < NL; ++k) {  // unconditional (clamped) loads: no early wait
             const int u = min(u0 + k * (NT - 64), max(n - 1, 0));
             const int vr = u >= k0 * IB_FIELDS ? 1 : 0;
-            a[k] = src[vr * var_stride + (u - vr * k0 * IB_FIELDS)];
+            const int uv = u - vr * k0 * IB_FIELDS;  // field uv % 28 of row uv / 28
+            const int off = (IB_STRIDE == IB_FIELDS) ? uv : (uv / IB_FIELDS) * IB_STRIDE + uv % IB_FIELDS;
+            a[k] = src[vr * var_stride + off];
         }
         if (t < 64 + 2 * HPE_DOF) {  // wave 1 draws rp, rg while the loads are in flight
             const int j = t - 64, d = j < HPE_DOF ? j : j - HPE_DOF;
@@ -402,14 +411,14 @@ __device__ __forceinline__ void pso_gen_body(const DevSwarm &sw, const DevObs *_
         }
         const unsigned long long gcell = gmin_load(sw, g - 1);
         const Sig pv = sw.sig[g > 1 ? g - 1 : 0];
-        if (sw.ext) exr = sw.ext[t <= HPE_DOF ? t : HPE_DOF];
+        if (XCH) exr = sw.ext[t <= HPE_DOF ? t : HPE_DOF];
         const double fmin = gmin_reduce(gcell);  // NaN when no value was written
         // informant = first argmin of pbest cost over {i} U incoming (PSO.cpp:810-812),
         // under BOTH variants while the gmin reduction is in flight (independent chains):
         // rebuilt = topology g, kept = the topology of g-1 (pv.topo); the decision below
         // only selects.  Candidates in lanes 0..k-1, self in lane 15 (K <= 15: one 16-lane
         // row) or 63.
-        const int self_lane = (K <= 15) ? 15 : 63;
+        const int self_lane = ROW16 ? 15 : 63;
         int infv[2], islv[2];
         double infc[2];
 #pragma unroll
@@ -421,8 +430,8 @@ __device__ __forceinline__ void pso_gen_body(const DevSwarm &sw, const DevObs *_
             double v = ok ? tc[vr] : (self ? pci : __builtin_inf());
             const int idx = ok ? (int)(tag & 0xffffffff) : (self ? i : 0x7fffffff);
             if (v != v) v = __builtin_inf();
-            if (K <= 15) row0_argmin_lex(v, idx, ok ? t : -1, infv[vr], islv[vr], &infc[vr]);
-            else wave_argmin_lex(v, idx, ok ? t : -1, infv[vr], islv[vr], &infc[vr]);
+            if (ROW16) row0_argmin_lex(v, idx, ok ? t : -1, infv[vr], islv[vr], XCH ? &infc[vr] : nullptr);
+            else wave_argmin_lex(v, idx, ok ? t : -1, infv[vr], islv[vr], XCH ? &infc[vr] : nullptr);
         }
         BLK_TS(g, 6);
         // end-of-generation update of g-1 (PSO.cpp:864-877) / initial gbest (:755-760),
@@ -450,7 +459,7 @@ __device__ __forceinline__ void pso_gen_body(const DevSwarm &sw, const DevObs *_
         inf = var ? infv[1] : infv[0];
         islot = var ? islv[1] : islv[0];
         // the exchanged candidate (index "P": after every local one) wins only strictly
-        if (sw.ext) use_ext = readlane_f64(exr, HPE_DOF) < (var ? infc[1] : infc[0]);
+        if (XCH) use_ext = readlane_f64(exr, HPE_DOF) < (var ? infc[1] : infc[0]);
         if (t < HPE_DOF) sm.pbr[t] = pbi;  // for the pushing waves, if x does not improve
         BLK_TS(g, 7);
         sc.lap(1);
@@ -497,7 +506,9 @@ __device__ __forceinline__ void pso_gen_body(const DevSwarm &sw, const DevObs *_
     // ---- evaluation and pbest (PSO.cpp:848-861)
     double fx = eval_block<EV_COST, NT, false>(sm, o, cv, H, nullptr, pre, g, &own0, slice == 0);
     BLK_TS(g, 4);
-    if (SPLIT > 1 && !split_arrive<SPLIT>(sw, g, i, slice, fx, sm)) return;
+    if constexpr (SPLIT > 1) {
+        if (!split_arrive<SPLIT>(sw, g, i, slice, fx, sm)) return;
+    }
     sc.start();
     const bool better = fx < pci;
     const double pn = better ? fx : pci;
@@ -516,11 +527,19 @@ __device__ __forceinline__ void pso_gen_body(const DevSwarm &sw, const DevObs *_
     sc.span(5);
 }
 
+template <bool ROW16>
 __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *__restrict__ og,
                                                     const DevHand *__restrict__ Hg, int g,
                                                     double W1, double C1, double C2,
                                                     InboxCounts kin) {
-    pso_gen_body<HPE_NT, 1>(sw, og, Hg, g, W1, C1, C2, kin);
+    pso_gen_body<HPE_NT, 1, false, ROW16>(sw, og, Hg, g, W1, C1, C2, kin);
+}
+template <bool ROW16>
+__global__ __launch_bounds__(HPE_NT) void k_pso_gen_x(DevSwarm sw, const DevObs *__restrict__ og,
+                                                      const DevHand *__restrict__ Hg, int g,
+                                                      double W1, double C1, double C2,
+                                                      InboxCounts kin) {
+    pso_gen_body<HPE_NT, 1, true, ROW16>(sw, og, Hg, g, W1, C1, C2, kin);
 }
 
 // Large clouds (N > RF_STAGE_MAX, e.g. the full ~9.3k-point cloud): SPLIT workgroups of 256
@@ -534,13 +553,13 @@ __global__ __launch_bounds__(PSO_SPLIT_NT, 3) void k_pso_init_split(DevSwarm sw,
                                                                    const DevHand *__restrict__ Hg) {
     pso_init_body<PSO_SPLIT_NT, SPLIT>(sw, x0, og, Hg);
 }
-template <int SPLIT>
+template <int SPLIT, bool XCH, bool ROW16>
 __global__ __launch_bounds__(PSO_SPLIT_NT, 3) void k_pso_gen_split(DevSwarm sw,
                                                                   const DevObs *__restrict__ og,
                                                                   const DevHand *__restrict__ Hg,
                                                                   int g, double W1, double C1,
                                                                   double C2, InboxCounts kin) {
-    pso_gen_body<PSO_SPLIT_NT, SPLIT>(sw, og, Hg, g, W1, C1, C2, kin);
+    pso_gen_body<PSO_SPLIT_NT, SPLIT, XCH, ROW16>(sw, og, Hg, g, W1, C1, C2, kin);
 }
 
 // ---------------------------------------------------------------- wave-per-particle form
@@ -624,6 +643,7 @@ __global__ __launch_bounds__(PW_NT) void k_pso_init_w(DevSwarm sw, const double 
     for (int k = 0; k < 3; ++k) push_inbox_w(sw, 0, i, l + 64 * k, lk[k], 1, c, f.th);
 }
 
+template <bool XCH, bool ROW16>
 __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *__restrict__ og,
                                                      const DevHand *__restrict__ Hg, int g,
                                                      double W1, double C1, double C2) {
@@ -665,7 +685,7 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
     }
     const unsigned long long gcell = gmin_load(sw, g - 1);
     const Sig pv = sw.sig[g > 1 ? g - 1 : 0];
-    const double exr = sw.ext ? sw.ext[l <= HPE_DOF ? l : HPE_DOF] : 0.0;  // exchange (sw.ext)
+    const double exr = XCH ? sw.ext[l <= HPE_DOF ? l : HPE_DOF] : 0.0;  // exchange (sw.ext)
     // the draws while the loads are in flight
     const int dl = l < HPE_DOF ? l : 0;
     const double rp = philox_u01(sw.seed, ST_RP, g, ic, dl);
@@ -687,7 +707,7 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
     if (i == 0 && l == 0) sw.sig[g] = sg;
     const int topo = sg.topo, var = (topo == g) ? 1 : 0;
     // ---- informant (PSO.cpp:810-812)
-    const int self_lane = (K <= 15) ? 15 : 63;  // one 16-lane row when K <= 15
+    const int self_lane = ROW16 ? 15 : 63;  // one 16-lane row when K <= 15
     double v = __builtin_inf();
     int idx = 0x7fffffff, slot = -1;
     if (l < K) {
@@ -703,10 +723,10 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
     }
     if (v != v) v = __builtin_inf();
     int inf, islot;
-    double infc;
-    if (K <= 15) row0_argmin_lex(v, idx, slot, inf, islot, &infc);
-    else wave_argmin_lex(v, idx, slot, inf, islot, &infc);
-    const bool use_ext = sw.ext && readlane_f64(exr, HPE_DOF) < infc;  // strictly better
+    double infc = 0.0;
+    if (ROW16) row0_argmin_lex(v, idx, slot, inf, islot, XCH ? &infc : nullptr);
+    else wave_argmin_lex(v, idx, slot, inf, islot, XCH ? &infc : nullptr);
+    const bool use_ext = XCH && readlane_f64(exr, HPE_DOF) < infc;  // strictly better
     // ---- velocity, position, check_constraints (PSO.cpp:824-842, 358-377)
     if (l < HPE_DOF) {
         double vn;
@@ -1088,6 +1108,17 @@ __device__ __forceinline__ void gold_down(double a, double &b, double &alpha) {
 // after its evaluation with the same operations the serial search applies at that node
 // (its bracket state replayed from the round's start): the walk then follows byte codes
 // and reads one post-state instead of redoing the fp64 tests level by level.
+// Two round-4 variants of the Goldstein round, both exact, both measured no faster (A/B on
+// one box, 3 x 40 frames: refine 145.5 us with neither, 148.4 with both, 145.2 / 148.3
+// with one each): the nodes taking their own tests so the walk follows byte
+// codes (HPE_GOLD_CODED=1), and the rigid node as one fused function placing its matched
+// centres in registers (HPE_RIGID_FUSED=1).  Off by default.
+#ifndef HPE_GOLD_CODED
+#define HPE_GOLD_CODED 0
+#endif
+#ifndef HPE_RIGID_FUSED
+#define HPE_RIGID_FUSED 0
+#endif
 struct GoldIn {
     double fk, gp;  // f_k and g'p of the search
     double a, b, al;  // this node's bracket state before its test (al = its alpha)
@@ -1216,7 +1247,7 @@ __device__ __forceinline__ void eval_nodes(RefineSm &rs, int nn, const DevObs &o
         if (w < nn) {
             wave_sync();
             double f;
-            if (RIGID && fp) {  // small clouds: the fused node (no LDS round trip inside)
+            if (RIGID && fp && HPE_RIGID_FUSED) {  // small clouds: the fused node
                 f = rblk ? rigid_node<RG_TRANS>(rs.w[w], o, cv, H, rs.rg, *thr, *fp)
                          : rigid_node<RG_ROT>(rs.w[w], o, cv, H, rs.rg, *thr, *fp);
             } else if (RIGID) {
@@ -1475,8 +1506,42 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
             thl = rs.x0[l < HPE_DOF ? l : 0] + gin.al * pl;
             if (l < HPE_DOF) rs.w[w].th[l] = thl;
         }
-        eval_nodes<MW, RIGID>(rs, nn, o, cv, H, match, Xt, ml, flag, &thl, fp, rblk, &gin);
+        eval_nodes<MW, RIGID>(rs, nn, o, cv, H, match, Xt, ml, flag, &thl, fp, rblk,
+                              HPE_GOLD_CODED ? &gin : nullptr);
         if (MW && ml->failed) break;  // the launch is ending early (DevMw::err)
+#if !HPE_GOLD_CODED
+        // the serial rules walked level by level on the nodes' costs
+        int node = 0;
+        accepted = -1;
+#pragma unroll
+        for (int lev = 0; lev < 6; ++lev) {  // the deepest shape path is 6 nodes
+            if (node >= 15 || done) break;
+            if (it >= 30) {
+                done = true;
+                tk = 0;
+                break;
+            }
+            ++it;
+            const double f1 = rs.f[node];
+            const double armijo = fk + 0.25 * alpha * gp;
+            const double gold = fk + (1 - 0.25) * alpha * gp;
+            if (f1 <= armijo) {
+                if (f1 >= gold) {
+                    tk = alpha;
+                    done = true;
+                    accepted = node;
+                } else {
+                    gold_up(A, B, alpha);
+                    node = (int)((sh.up >> (4 * node)) & 15u);
+                    ctx = 2;
+                }
+            } else {
+                gold_down(A, B, alpha);
+                node = (int)((sh.dn >> (4 * node)) & 15u);
+                ctx = 1;
+            }
+        }
+#else
         // the walk: every node took its own test (gold_decide), so the serial search's path
         // through the shape is a chain of byte codes; the bracket state after the round is
         // the post-state of the last node tested
@@ -1515,6 +1580,7 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
             B = rs.gpost[lastn][1];
             alpha = rs.gpost[lastn][2];
         }
+#endif
         if (!done && it >= 30) done = true;  // tk stays 0
         // x0 is read only before eval_nodes' barrier in a round
         if (UPD && done && t < HPE_DOF) rs.x0[t] = rs.x0[t] - tk * gl;

@@ -56,6 +56,11 @@ struct Sig {  // swarm scalars carried across generation kernels
 // topologies of generation g+1 (rebuilt at g+1, or kept), so generation g+1 reads all
 // it needs from its own inbox in one round trip.
 #define IB_FIELDS 28  // tag, pbest cost, pbest position[26]
+// doubles between consecutive inbox rows in HBM: 28 packs the rows (a 224-B row straddles
+// 128-B lines); 32 starts every row on a line (two lines per row)
+#ifndef IB_STRIDE
+#define IB_STRIDE 28
+#endif
 #define GMIN_SHARDS 32  // atomicMin cells per generation
 #define GMIN_STRIDE 16  // u64 per cell: one 128-B line each
 struct DevSwarm {
@@ -63,7 +68,7 @@ struct DevSwarm {
     double *pch;              // (G+1) x P        pbest costs per generation
     double *pb;               // P x 26           pbest positions (own particle only)
     double *v;                // P x 26           velocities (own particle only)
-    double *inbox;            // 2 x 2 x P x K x IB_FIELDS  [g&1][kept, rebuilt][receiver][slot]
+    double *inbox;            // 2 x 2 x P x K x IB_STRIDE  [g&1][kept, rebuilt][receiver][slot]
     double *ibtc;             // 2 x 2 x P x K x {tag, cost}  (wave form: compact informant costs)
     unsigned long long *gmin; // (G+1) x GMIN_SHARDS cells (128-B apart): min pbest cost bits
                               // per generation, particle i lowering shard i % GMIN_SHARDS

@@ -9,6 +9,7 @@ the files committed under profiles/:
 
 usage: prof_summary.py stats RUN_DIR OUT.csv
        prof_summary.py pmc FETCH_DIR WRITE_DIR KERNEL P N OUT.json
+       prof_summary.py counters RUN_DIR KERNEL COUNTER...   (per-dispatch averages, JSON)
 """
 import csv
 import glob
@@ -90,8 +91,19 @@ def pmc(fetch_dir, write_dir, kernel, P, N, out):
     print(json.dumps(res, indent=1))
 
 
+def counters(run_dir, kernel, names):
+    match = lambda n: short(n) == kernel or short(n).startswith(kernel + "<")  # noqa: E731
+    res = {"kernel": kernel}
+    for c in names:
+        v = [x for n, x in counter_rows(run_dir, c) if match(n)]
+        res[c] = {"dispatches": len(v), "avg": sum(v) / len(v) if v else None}
+    print(json.dumps(res))
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "stats":
         stats(sys.argv[2], sys.argv[3])
+    elif sys.argv[1] == "counters":
+        counters(sys.argv[2], sys.argv[3], sys.argv[4:])
     else:
         pmc(sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5]), int(sys.argv[6]), sys.argv[7])
