@@ -1,12 +1,13 @@
 #!/bin/bash
-# gpurun with retries on infrastructure failures that happen before the command runs
-# usage: tools/gpurun_retry.sh LOG TIMEOUT 'command'
+# gpurun with retries when the call never ran: an infrastructure failure while the box
+# was prepared, a back-off, or no free GPU slot (exit 3).  A command that ran is never
+# repeated.  usage: tools/gpurun_retry.sh LOG TIMEOUT 'command'
 LOG=$1; TO=$2; CMD=$3
-for a in 1 2 3 4; do
+for a in 1 2 3 4 5 6 7 8; do
   timeout $((TO + 1200)) /usr/local/graft/bin/gpurun --timeout $TO -- "$CMD" > $LOG 2>&1
   rc=$?
-  if grep -q "stopped responding while being prepared\|backing off\|status=transient" $LOG || [ $rc -eq 3 ]; then
-    echo "[retry $a after infra failure rc=$rc]" >> $LOG.retries; sleep 45; continue
+  if [ $rc -eq 3 ] || grep -q "stopped responding while being prepared\|backing off\|status=transient" $LOG; then
+    echo "[retry $a: the call did not run, rc=$rc]" >> $LOG.retries; sleep 120; continue
   fi
   break
 done
