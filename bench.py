@@ -83,10 +83,14 @@ def parse():
     ap.add_argument("--resident", action="store_true",
                     help="preprocess every frame before timing (default: each step prepares "
                          "the next frame from host depth on the GPU, overlapped)")
-    ap.add_argument("--frames-per-graph", type=int, default=0,
-                    help="with --resident: track the frames through the offline sequence API "
-                         "(hpe_track_sequence_dev), this many frames per graph launch "
-                         "(default 0: one hpe_track_frame_dev graph per frame)")
+    ap.add_argument("--frames-per-graph", type=int, default=None,
+                    help="frames captured per graph launch: the raw depth frames resident in "
+                         "HBM, each next frame prepared inside the previous frame's refine "
+                         "launch (hpe_track_raw_sequence_dev); with --resident the prepared "
+                         "frames through hpe_track_sequence_dev.  0: one graph per frame "
+                         "(hpe_track_pipelined from host frames / hpe_track_frame_dev).  "
+                         "Default: 8 on one GPU, 0 with N > 1 (the per-frame exchange sits "
+                         "between frames), --dump or --exchange gen:K")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--seed", type=int, default=TRAJ_SEED, help="trajectory seed")
@@ -110,8 +114,10 @@ def parse():
                          "as .npy under this directory")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)
     a = ap.parse_args()
-    if a.frames_per_graph and not (a.resident and a.gpus == 1 and not a.dump):
-        ap.error("--frames-per-graph needs --resident, one GPU and no --dump "
+    if a.frames_per_graph is None:
+        a.frames_per_graph = 8 if (a.gpus == 1 and not a.dump and a.exchange == "frame") else 0
+    if a.frames_per_graph and not (a.gpus == 1 and not a.dump):
+        ap.error("--frames-per-graph needs one GPU and no --dump "
                  "(the per-frame exchange / dump sit between frames)")
     a.exchange_every = 0
     if a.exchange != "frame":
@@ -482,10 +488,21 @@ def main():
             np.save(os.path.join(args.dump, "x0.npy"), state[:26].cpu().numpy())
     K = args.frames_per_graph
 
-    def run_sequence(first, n):  # offline: frames first .. first+n-1, K per graph launch
-        ctx.track_sequence(P, refine, state.data_ptr(), first, n, K)
+    d_raw = None
+    if K and not args.resident:  # the raw frames resident in HBM before the timed region
+        d_raw = torch.from_numpy(np.ascontiguousarray(np.stack(raw), dtype=np.float32)).to(
+            f"cuda:{local}")
+        torch.cuda.synchronize()
 
-    if not args.resident:
+    def run_sequence(first, n):  # frames first .. first+n-1, K per graph launch
+        if args.resident:  # prepared frames (offline sequence API)
+            ctx.track_sequence(P, refine, state.data_ptr(), first, n, K)
+        else:  # raw frames, each next one prepared inside the previous frame's refine launch
+            ctx.track_raw_sequence(P, refine, state.data_ptr(),
+                                   d_raw.data_ptr() + first * d_raw[0].numel() * 4, n, True, ds,
+                                   frames_per_graph=K)
+
+    if not args.resident and not K:
         ctx.pipeline_begin(raw[0], True, ds)
     if K:
         run_sequence(0, args.warmup)
@@ -537,7 +554,7 @@ def main():
           for _ in range(args.steps)]
     state.copy_(state0)
     torch.cuda.synchronize()
-    if not args.resident:
+    if not args.resident and not K:
         ctx.pipeline_begin(raw[args.warmup], True, ds)
     if K:  # one event pair around the whole sequence
         ev[0][0].record(ext)
@@ -652,9 +669,15 @@ def main():
                                     "next_frame preprocessing (GPU, fused into the refine "
                                     "launch) + ") + "refine_init_pose + pso_evolve + "
                                     "cal_cost(bestp)" + (
-                                        f"; frames resident in HBM, tracked by the offline "
-                                        f"sequence API, {K} frames per graph launch" if K
-                                        else "")),
+                                        f"; prepared frames resident in HBM, tracked by the "
+                                        f"offline sequence API, {K} frames per graph launch"
+                                        if K and args.resident else
+                                        f"; raw float32 mm depth frames resident in HBM, "
+                                        f"hpe_track_raw_sequence_dev, {K} frames per graph "
+                                        f"launch" if K else
+                                        "" if args.resident else
+                                        "; raw frames from host memory (zero-copy over "
+                                        "PCIe), one hpe_track_pipelined graph per frame")),
                        "frames_per_graph": K or 1,
                        "particles": P, "generations": G, "maxiter": G + 1,
                        "trajectory": (None if args.frames else

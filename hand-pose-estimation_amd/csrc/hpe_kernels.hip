@@ -1015,9 +1015,11 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
         if (obs_out && t < (int)(sizeof(DevObs) / 8)) ((unsigned long long *)obs_out)[t] = obs_word;
         if (seq_cur) {
             // the next frame's descriptor for the next frame's kernels (stream order: they
-            // start after this kernel); the slot after the last is never read
+            // start after this kernel); the slot after the last is never read.  No table
+            // (resident raw sequences): the row alone advances -- the next frame's refine
+            // launch prepares raw frame row + 1 by it
             const int nx = seq_slot + 1 < HPE_MAX_SLOTS ? seq_slot + 1 : seq_slot;
-            if (t < (int)(sizeof(DevObs) / 8))
+            if (seq_table && t < (int)(sizeof(DevObs) / 8))
                 ((unsigned long long *)seq_obs)[t] = ((const unsigned long long *)(seq_table + nx))[t];
             if (t == 0) {
                 seq_cur[0] = seq_slot + 1;

@@ -49,6 +49,11 @@ struct PrepArgs {
     PrepInfo *info;
     DevObs *obs_out;
     unsigned *ctr;  // [0] bands arrived, [1] (merged cloud, DT) arrived, [2] DT has its mask
+    // resident raw sequences (hpe_track_raw_sequence_dev): raw is the sequence's first frame
+    // and the frame prepared is the one after the device row cursor's (*raw_row + 1), so a
+    // captured chunk graph serves every chunk; null: raw is the frame itself
+    const int *raw_row;
+    unsigned long long raw_stride;  // floats per raw frame
 };
 
 // LDS layout: chunk[PREP_CH] doubles | acc1, flag (64 B) | wcnt, hcnt | mask bits | wmax
@@ -484,8 +489,10 @@ __device__ __forceinline__ void prep_write_descriptor(const PrepArgs &a) {
 
 // One preparing workgroup (index g in [0, PREP_WG)); the last to finish writes the
 // descriptor.
-__device__ __forceinline__ void prep_workgroup(const PrepArgs &a, int g, unsigned char *lds) {
+__device__ __forceinline__ void prep_workgroup(const PrepArgs &a0, int g, unsigned char *lds) {
     int *flag = (int *)(lds + PREP_CH * 8 + 8);
+    PrepArgs a = a0;
+    if (a0.raw_row) a.raw = a0.raw + (size_t)(*a0.raw_row + 1) * a0.raw_stride;
     if (g < PREP_BANDS) {
         prep_band(a, g, lds);
         if (!prep_arrive_last(a.ctr, PREP_BANDS, flag)) return;

@@ -131,6 +131,17 @@ class Context:
             self._h, int(num_p), int(refine), C.c_void_p(d_state_ptr), int(first_slot), int(n),
             int(frames_per_graph), C.c_void_p(d_hist_ptr) if d_hist_ptr else None))
 
+    def track_raw_sequence(self, num_p, refine, d_state_ptr, d_raw_ptr, n, to_cm=True,
+                           downsample=True, focal=241.42, frames_per_graph=0, d_hist_ptr=None):
+        """Track n raw depth frames resident in HBM (d_raw_ptr: n x 240x320 float mm) in
+        order (test_full's loop), each next frame prepared inside the previous frame's
+        refine launch, frames_per_graph per graph launch; frame f's {bestp, cost} to
+        d_hist_ptr + 27 f (device, optional).  Asynchronous on the context stream."""
+        self.check(self.lib.hpe_track_raw_sequence_dev(
+            self._h, int(num_p), int(refine), C.c_void_p(d_state_ptr), C.c_void_p(d_raw_ptr),
+            int(n), int(to_cm), int(downsample), float(focal), int(frames_per_graph),
+            C.c_void_p(d_hist_ptr) if d_hist_ptr else None))
+
     def frame_readback(self, slot):
         depth = np.zeros((IMG_H, IMG_W)); dt = np.zeros((IMG_H, IMG_W), dtype=np.float32)
         cloud = np.zeros((IMG_H * IMG_W, 3)); n = C.c_int32(0)

@@ -52,6 +52,9 @@ SIGNATURES = {
     "hpe_frame_readback": (C.c_int, [C.c_void_p, C.c_int, dp, fp, dp, ip, dp, dp]),
     "hpe_pipeline_begin": (C.c_int, [C.c_void_p, fp, C.c_int, C.c_int, C.c_double]),
     "hpe_track_pipelined": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, fp]),
+    "hpe_track_raw_sequence_dev": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p,
+                                             C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_double,
+                                             C.c_int, C.c_void_p]),
     "hpe_build_spheres": (C.c_int, [C.c_void_p, dp, C.c_int, dp, dp]),
     "hpe_eval_costs": (C.c_int, [C.c_void_p, dp, C.c_int, C.c_int, dp, ip]),
     "hpe_cal_cost2": (C.c_int, [C.c_void_p, dp, ip, C.c_int, dp, dp]),

@@ -229,6 +229,20 @@ int hpe_pipeline_begin(hpe_ctx *ctx, const float *depth_mm, int to_cm, int downs
 int hpe_track_pipelined(hpe_ctx *ctx, int num_p, int refine, double *d_state,
                         const float *next_depth_mm);
 
+/* Resident raw sequence: test_full's loop (testmodel.cpp:117-139) over n raw depth frames
+ * already in HBM -- d_raw_mm: device, n x 240x320 float mm, frame after frame -- with
+ * next_frame (observedmodel.cpp:420-430) of frame f+1 inside frame f's refine launch, as
+ * hpe_track_pipelined does, and frames_per_graph frames (0: HPE_SEQ_CHUNK) captured into one
+ * graph, so the graph-to-graph gap is paid once per chunk.  The preparation reads its raw
+ * frame through a device row cursor that each frame's final kernel advances: a captured
+ * chunk serves every chunk of the same shape.  Frame 0 is prepared first, on the same
+ * stream.  d_state: 27 device doubles {x0 -> bestp, cost} carried from frame to frame;
+ * d_hist (device, optional): n x 27 doubles, frame f's {bestp, cost}.  Asynchronous on
+ * hpe_stream(ctx); ends a pipelined sequence in progress. */
+int hpe_track_raw_sequence_dev(hpe_ctx *ctx, int num_p, int refine, double *d_state,
+                               const float *d_raw_mm, int n, int to_cm, int downsample,
+                               double focal, int frames_per_graph, double *d_hist);
+
 /* Kernel timing with HIP events on the context stream (bench instrumentation).
  * While enabled, every dispatch of the profiled kernels is launched through
  * hipExtLaunchKernel with a start/stop event pair (dispatch-packet timestamps: the

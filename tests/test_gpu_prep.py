@@ -191,3 +191,70 @@ def test_sequence_tracking_like_oracle_and_per_frame(gh, oracle, ora_hand, np_ha
     assert bad(gh.ctx.h, P, 1, C.c_void_p(st.data_ptr()), 4095, 2, 0, None) == hpe._lib.HPE_E_ARG
     assert bad(gh.ctx.h, P, 1, C.c_void_p(st.data_ptr()), s0, n, 33, None) == hpe._lib.HPE_E_ARG
     assert bad(gh.ctx.h, P, 1, None, s0, n, 0, None) == hpe._lib.HPE_E_ARG
+
+
+@pytest.mark.parametrize("downsample", [True, False])
+def test_raw_sequence_like_pipelined_and_oracle(gh, oracle, ora_hand, np_hand, downsample):
+    """hpe_track_raw_sequence_dev (raw frames resident in HBM, each next frame prepared inside
+    the previous frame's refine launch through the device row cursor, several frames per
+    graph): every frame's {bestp, cost} equals hpe_track_pipelined's frame by frame bit for
+    bit and the oracle's test_full loop, for chunks of 1, 3 (odd: both buffer parities,
+    ragged 3 + 3 + 1) and 8; graphs are keyed by chunk shape, so a replay captures none."""
+    import ctypes as C
+    import hpe
+    import torch
+    n = 7 if downsample else 3
+    P, maxiter = (32, 6) if downsample else (8, 3)
+    poses = hand_data.trajectory(n, seed=29)
+    depth = [oracle_np.render_depth_mm(np_hand, th) for th in poses]
+    ub, lb, sd = oracle_np.reference_bounds()
+    pso = hpe.PSO()
+    pso.set_pso_params(ub, lb, sd, 0.7298, 1.49618, 1.49618, maxiter, 1e-8, 1e-8)
+    pso._push(gh.ctx)
+    rt = gh.ctx.lib
+    st = torch.zeros(27, dtype=torch.float64, device="cuda:0")
+    st[:26] = torch.from_numpy(oracle_np.X0)
+    torch.cuda.synchronize()
+    gh.ctx.pipeline_begin(depth[0], downsample=downsample)
+    per_frame = []
+    for f in range(n):
+        gh.ctx.track_pipelined(P, 1, st.data_ptr(), depth[f + 1] if f + 1 < n else None)
+        gh.ctx.check(rt.hpe_sync(gh.ctx.h))
+        per_frame.append(st.cpu().numpy().copy())
+    per_frame = np.array(per_frame)
+    x_ref = oracle_np.X0.copy()
+    for f in range(n):
+        obs = oracle.preprocess(depth[f], downsample=downsample)
+        x_ref, _ = oracle.refine(ora_hand, obs, x_ref, rigid=REFINE_RIGID)
+        x_ref, _, _ = oracle.pso_evolve(ora_hand, obs, x_ref, P, maxiter, lb, ub, sd)
+        cr = oracle.cal_cost(ora_hand, obs, x_ref)
+        np.testing.assert_allclose(per_frame[f, :26], x_ref, rtol=0, atol=1e-6)
+        assert abs(per_frame[f, 26] - cr) <= 1e-8 * abs(cr)
+    d_raw = torch.from_numpy(np.stack(depth).astype(np.float32)).to("cuda:0")
+    hist = torch.empty((n, 27), dtype=torch.float64, device="cuda:0")
+    caps = C.c_uint64(0)
+    seen = set()
+    for K in (1, 3, 8, 3):  # the last: cached graphs
+        st[:26] = torch.from_numpy(oracle_np.X0)
+        st[26] = 0.0
+        hist.fill_(float("nan"))
+        torch.cuda.synchronize()
+        gh.ctx.check(rt.hpe_graph_captures(gh.ctx.h, C.byref(caps)))
+        before = caps.value
+        gh.ctx.track_raw_sequence(P, 1, st.data_ptr(), d_raw.data_ptr(), n,
+                                  downsample=downsample, frames_per_graph=K,
+                                  d_hist_ptr=hist.data_ptr())
+        gh.ctx.check(rt.hpe_sync(gh.ctx.h))
+        gh.ctx.check(rt.hpe_graph_captures(gh.ctx.h, C.byref(caps)))
+        assert np.array_equal(hist.cpu().numpy(), per_frame), K
+        assert np.array_equal(st.cpu().numpy(), per_frame[-1]), K
+        # one graph per chunk shape (length, first buffer's parity, last frame prepares more)
+        shapes = {(min(K, n - f0), f0 & 1, f0 + K < n) for f0 in range(0, n, K)}
+        assert caps.value - before == len(shapes - seen), (K, caps.value - before)
+        seen |= shapes
+    bad = rt.hpe_track_raw_sequence_dev
+    sp = C.c_void_p(st.data_ptr())
+    assert bad(gh.ctx.h, P, 1, sp, C.c_void_p(d_raw.data_ptr()), 0, 1, 1, 241.42, 0, None) == hpe._lib.HPE_E_ARG
+    assert bad(gh.ctx.h, P, 1, sp, None, n, 1, 1, 241.42, 0, None) == hpe._lib.HPE_E_ARG
+    assert bad(gh.ctx.h, P, 1, sp, C.c_void_p(d_raw.data_ptr()), n, 1, 1, 241.42, 33, None) == hpe._lib.HPE_E_ARG
+    assert bad(gh.ctx.h, P, 1, sp, C.c_void_p(d_raw.data_ptr()), n, 1, 1, 0.0, 0, None) == hpe._lib.HPE_E_ARG

@@ -1,0 +1,70 @@
+"""RCCL on the box: the multi-GPU exchange's collective (hpe.dist.exchange_best's
+all_gather_into_tensor) through torch.distributed's "nccl" backend (= RCCL on ROCm).  Only
+one GPU is available to the tests, and RCCL refuses two ranks on one device, so this runs
+a one-rank process group: it initialises an RCCL communicator on the device, tracks one
+frame with the HIP library, and all-gathers the tracker state on the tracker's own stream
+(as bench.py does per frame) -- the library, the communicator and the stream ordering are
+exercised on hardware; the N-rank logic itself is covered by the gloo tests."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+import hand_data
+
+pytestmark = pytest.mark.gpu
+
+SCRIPT = r'''
+import os, socket, sys
+import numpy as np
+import torch
+import torch.distributed as dist
+sys.path.insert(0, os.path.join(os.environ["HPE_ROOT"], "hand-pose-estimation_amd"))
+import hpe
+from hpe import synth
+torch.cuda.set_device(0)
+with socket.socket() as s:
+    s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]
+dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                        device_id=torch.device("cuda", 0))
+hand = hpe.reference_hand(device=0)
+ctx = hand.ctx
+ub, lb, sd = hpe.reference_bounds()
+pso = hpe.PSO()
+pso.set_pso_params(ub, lb, sd, 0.7298, 1.49618, 1.49618, 6, 1e-8, 1e-8)
+pso._push(ctx)
+poses = synth.trajectory(2, 0, revert=0.02)
+raw = [np.ascontiguousarray(ctx.render_depth(th)) for th in poses]
+state = torch.zeros(27, dtype=torch.float64, device="cuda:0")
+state[:26] = torch.from_numpy(poses[0])
+torch.cuda.synchronize()
+ctx.pipeline_begin(raw[0])
+ctx.track_pipelined(64, 1, state.data_ptr(), raw[1])
+ext = torch.cuda.ExternalStream(ctx.lib.hpe_stream(ctx.h), device="cuda:0")
+gathered = torch.zeros(27, dtype=torch.float64, device="cuda:0")
+with torch.cuda.stream(ext):
+    dist.all_gather_into_tensor(gathered, state)
+ctx.check(ctx.lib.hpe_sync(ctx.h))
+torch.cuda.synchronize()
+s, g = state.cpu().numpy(), gathered.cpu().numpy()
+assert np.isfinite(s).all() and np.array_equal(s, g), (s, g)
+v = torch.cuda.nccl.version()
+print("RCCL", ".".join(map(str, v)) if isinstance(v, tuple) else v, "backend", dist.get_backend(),
+      "cost", s[26])
+hand.ctx.close()
+dist.destroy_process_group()
+'''
+
+
+def test_rccl_one_rank_allgather_on_tracker_stream(tmp_path):
+    env = dict(os.environ, HPE_ROOT=str(hand_data.ROOT))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    f = tmp_path / "rccl1.py"
+    f.write_text(SCRIPT)
+    out = subprocess.run([sys.executable, str(f)], capture_output=True, text=True, timeout=240,
+                         env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "RCCL" in out.stdout and "backend nccl" in out.stdout, out.stdout
+    print(out.stdout.strip())
