@@ -5,7 +5,7 @@ O=gpurun_out/${1:-r04_launch}
 mkdir -p $O
 U=tools/ubench_launch
 {
-for d in 0 1; do
+for d in 0 1 2; do
   for B in 1 256; do
     echo "== default"; timeout -k 5 60 $U $B 30 $d || exit 1
     echo "== DEBUG_CLR_GRAPH_PACKET_CAPTURE=0"; DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 timeout -k 5 60 $U $B 30 $d || exit 1

@@ -14,7 +14,9 @@ __global__ __launch_bounds__(512) void k_step(const unsigned *__restrict__ in, u
     __shared__ unsigned s;
     if (t == 0) s = in[(b * 7 + g) % gridDim.x];
     __syncthreads();
-    if (dirty) scratch[((size_t)b * 512 + t) % (1 << 17)] = (double)(s + g);  // 1 MB of lines
+    if (dirty == 1) scratch[((size_t)b * 512 + t) % (1 << 17)] = (double)(s + g);  // 1 MB of lines
+    if (dirty == 2)  // the same stores, nontemporal
+        __builtin_nontemporal_store((double)(s + g), &scratch[((size_t)b * 512 + t) % (1 << 17)]);
     if (t == 0) out[b] = s + 1;
 }
 
