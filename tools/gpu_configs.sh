@@ -1,6 +1,7 @@
 # BASELINE configs on one GPU, each its own bench.py run: N = full
 # cloud, the 400-frame sequence (config 3), 4096 x 40 (config 4), 32 x 10 (config 1's
-# shape), one 1024-particle subswarm of config 5, the resident-frames variant.
+# shape), one 1024-particle subswarm of config 5, the per-frame pipelined loop (raw frames
+# from host memory: the N > 1 form), prepared frames resident per frame / 8 per graph.
 set -o pipefail
 O=gpurun_out/${1:-r02}/configs
 rm -rf $O; mkdir -p $O
@@ -9,5 +10,6 @@ timeout -k 10 300 python bench.py --steps 400 --warmup 1 --no-cpu-baseline > $O/
 timeout -k 10 300 python bench.py --config p4096 --no-cpu-baseline > $O/p4096.log 2>&1 && \
 timeout -k 10 300 python bench.py --config p32 --no-cpu-baseline > $O/p32.log 2>&1 && \
 timeout -k 10 300 python bench.py --config subswarm8 --no-cpu-baseline > $O/subswarm1.log 2>&1 && \
-timeout -k 10 300 python bench.py --resident --no-cpu-baseline > $O/resident.log 2>&1 && \
+timeout -k 10 300 python bench.py --frames-per-graph 0 --no-cpu-baseline > $O/pipelined.log 2>&1 && \
+timeout -k 10 300 python bench.py --resident --frames-per-graph 0 --no-cpu-baseline > $O/resident.log 2>&1 && \
 timeout -k 10 300 python bench.py --resident --frames-per-graph 8 --no-cpu-baseline > $O/resident_seq8.log 2>&1
