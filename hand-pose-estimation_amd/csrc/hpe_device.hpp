@@ -873,6 +873,10 @@ struct Pt {
 typedef _Float16 hpe_h8 __attribute__((ext_vector_type(8)));
 typedef float hpe_f16x __attribute__((ext_vector_type(16)));
 #define MF_BIAS 1.0f
+// the allowance for fp16 subnormals flushed by the unit (3.6 2^-14 per cm of S)
+#ifndef MF_FLUSH
+#define MF_FLUSH 0x1p-11f
+#endif
 struct MfmaSph {
     hpe_h8 a0, a1;     // sphere fragments: tile 0 = spheres 0..31, tile 1 = 32..47 (+ zero rows)
     float ox, oy, oz;  // the origin: sphere 0's fp32 centre
@@ -928,7 +932,8 @@ __device__ __forceinline__ MfmaSph mfma_sph(const FkSm &f) {
 // point): the match of point r (bf_search's, both lanes of the pair get it).  q*: the
 // point's fp32 coordinates.  Returns -1 where bf_search must decide (the caller sends the
 // wave's tile there, wave-uniformly).
-__device__ __forceinline__ int mfma_match(const MfmaSph &m, float qx, float qy, float qz) {
+__device__ __forceinline__ int mfma_match(const FkSm &f, const MfmaSph &m, float qx, float qy,
+                                          float qz) {
     const int l = threadIdx.x & 63, h = l >> 5;
     const float px = qx - m.ox, py = qy - m.oy, pz = qz - m.oz;
     const float pp = (px * px + py * py) + pz * pz;
@@ -980,9 +985,36 @@ __device__ __forceinline__ int mfma_match(const MfmaSph &m, float qx, float qy, 
     const unsigned F1 = min(M1, P1), F2 = umed3(M1, P1, min(M2, P2));
     const float v1 = __uint_as_float(F1 & 0xFFFFFFC0u), v2 = __uint_as_float(F2 & 0xFFFFFFC0u);
     const float S = sqrtf(pp) * 1.000001f + m.C;
-    const float M = ((0x1p-18f * S) * S + 0x1p-11f * S) + (0x1p-16f * v1 + 0x1p-17f) + 0x1p-20f * v2;
-    const bool ok = (S < 250.f) && (v2 - v1 > M) && v1 > 0.f;  // false for NaN
-    return ok ? (int)(F1 & 63u) : -1;
+    const float Mb = ((0x1p-18f * S) * S + MF_FLUSH * S) + (0x1p-16f * v1 + 0x1p-17f);
+    const bool fin = (S < 250.f) && v1 > 0.f;  // false for NaN
+    const bool single = fin && (v2 - v1 > Mb + 0x1p-20f * v2);
+    if (!__ballot(!single)) return (int)(F1 & 63u);  // the common case: every point decided
+    // a point of this wave has a second sphere within M: if the third smallest is clear of
+    // M, the two smallest are the only candidates and their fp32 d^2 (bf_search's
+    // operations) decide -- BFMatcher's match is the first candidate within the sqrt class
+    // of their minimum.  Three or more candidates: -1 (bf_search).
+    asm volatile("" ::: "memory");  // keeps this rare path's work out of the common one
+    unsigned t3 = ~0u;
+#pragma unroll
+    for (int k = 0; k < 24; ++k) {
+        const unsigned kg = key[k] + 4u * (unsigned)h;
+        t3 = min(t3, kg > F2 ? kg : ~0u);
+    }
+    const unsigned T3 = min(t3, mf_xor32_u(t3));
+    const float v3 = __uint_as_float(T3 & 0xFFFFFFC0u);
+    const bool pair = fin && !single && (v3 - v1 > Mb + 0x1p-20f * v3);
+    int idx = single ? (int)(F1 & 63u) : -1;
+    if (pair) {
+        const int j1 = (int)(F1 & 63u), j2 = (int)(F2 & 63u);
+        const float t1x = qx - f.Sp[0][j1], t1y = qy - f.Sp[1][j1], t1z = qz - f.Sp[2][j1];
+        const float t2x = qx - f.Sp[0][j2], t2y = qy - f.Sp[1][j2], t2z = qz - f.Sp[2][j2];
+        const float D1 = (t1x * t1x + t1y * t1y) + t1z * t1z;
+        const float D2 = (t2x * t2x + t2y * t2y) + t2z * t2z;
+        const float hi = hi_sqrt_class(fminf(D1, D2));
+        const int a = min(j1, j2), b = max(j1, j2);
+        idx = ((a == j1 ? D1 : D2) <= hi) ? a : b;
+    }
+    return idx;
 }
 template <class CV>
 __device__ __forceinline__ Pt load_pt(const CV &cv, int it) {
@@ -1028,8 +1060,9 @@ __device__ __forceinline__ double search_align(const FkSm &f, const CV &cv,
             const int pn = min(p + 32 * tstride, cv.n - 1);
             const double Xn = cv.cx[pn], Yn = cv.cy[pn], Zn = cv.cz[pn];
             const float qx = (float)X, qy = (float)Y, qz = (float)Z;
-            int idx = mfma_match(ms, qx, qy, qz);
+            int idx = mfma_match(f, ms, qx, qy, qz);
             if (__ballot(idx < 0)) {
+                asm volatile("" ::: "memory");  // (none of this ahead of the branch)
                 // bf_search for the wave's 32 points in its own layout (lanes 2j, 2j + 1:
                 // point j, sphere halves 0 / 1), the result moved to lane j (and j + 32)
                 const int h2 = l & 1, pj = min(32 * tile + (l >> 1), cv.n - 1);

@@ -32,7 +32,7 @@ __global__ __launch_bounds__(64) void k_check(const float *__restrict__ sph, con
     unsigned bad = 0, fall = 0;
     for (int tile = 0; tile < PTS / 32; ++tile) {
         const float *p = pts + ((size_t)b * PTS + 32 * tile + r) * 3;
-        const int idx = mfma_match(ms, p[0], p[1], p[2]);
+        const int idx = mfma_match(f, ms, p[0], p[1], p[2]);
         const int h2 = l & 1;
         const float *q = pts + ((size_t)b * PTS + 32 * tile + (l >> 1)) * 3;
         const BfOut rb = bf_search(f, H, f.Sp[0] + 24 * h2, f.Sp[1] + 24 * h2, f.Sp[2] + 24 * h2,
@@ -78,7 +78,7 @@ __global__ __launch_bounds__(512) void k_time(const float *__restrict__ sph, con
         const MfmaSph ms = mfma_sph(f);
         for (int tile = w; tile < PTS / 32; tile += 8) {
             const float *p = pts + ((size_t)b * PTS + 32 * tile + r) * 3;
-            acc += mfma_match(ms, p[0], p[1], p[2]);
+            acc += mfma_match(f, ms, p[0], p[1], p[2]);
         }
     } else {
         for (int tile = w; tile < PTS / 32; tile += 8) {
