@@ -651,9 +651,19 @@ __device__ __forceinline__ DepthG depth_issue_at(const SphXYZ &c, int i, const D
                                                  const DevHand *__restrict__ H) {
     i = i < HPE_NS ? i : HPE_NS - 1;
     const double x = c.x, y = c.y * -1, z = c.z * -1;
-    const double pu = (o.K[0] * x + o.K[1] * y) + o.K[2] * z;
-    const double pv = (o.K[3] * x + o.K[4] * y) + o.K[5] * z;
-    const double pw = (o.K[6] * x + o.K[7] * y) + o.K[8] * z;
+    double pu, pv, pw;
+    if (o.K[1] == 0.0 && o.K[3] == 0.0 && o.K[6] == 0.0 && o.K[7] == 0.0 && o.K[8] == 1.0) {
+        // the pinhole K of every frame (focal, principal point): the zero terms only add a
+        // signed zero, which changes no value here; a non-finite coordinate leaves the
+        // sphere off-image either way (general form: pw NaN, this form: dx or dy non-finite)
+        pu = o.K[0] * x + o.K[2] * z;
+        pv = o.K[4] * y + o.K[5] * z;
+        pw = z;
+    } else {
+        pu = (o.K[0] * x + o.K[1] * y) + o.K[2] * z;
+        pv = (o.K[3] * x + o.K[4] * y) + o.K[5] * z;
+        pw = (o.K[6] * x + o.K[7] * y) + o.K[8] * z;
+    }
     const double dx = floor(pu / pw), dy = floor(pv / pw);
     DepthG d;
     d.in = dx >= 0 && dx < HPE_IMG_W && dy >= 0 && dy < HPE_IMG_H;  // NaN: off-image
