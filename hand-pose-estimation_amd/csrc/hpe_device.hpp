@@ -186,8 +186,11 @@ __device__ __forceinline__ void wave_sync() {
 // on a branch the cost terms' squared distances practically never enter (callers with
 // several roots fix them up behind ONE branch, so the roots stay one basic block).
 // tools/sqrt_check.hip compares hpe_sqrt with sqrt bitwise.
+// (2^-767 <= x < inf as two integer operations on the high word: both bounds have a zero
+// low word, and negative values, -0 and NaN fall outside the unsigned range)
 __device__ __forceinline__ bool hpe_sqrt_direct(double x) {
-    return x >= 0x1p-767 && x < __builtin_inf();
+    const unsigned hi = (unsigned)((unsigned long long)__double_as_longlong(x) >> 32);
+    return hi - 0x10000000u < 0x7FF00000u - 0x10000000u;
 }
 __device__ __forceinline__ double hpe_sqrt_nr(double x) {
     const double y = __builtin_amdgcn_rsq(x);
@@ -555,18 +558,22 @@ struct __align__(16) RigidSm {
     double C;             // self_collision_penalty (costfunc.cpp:130-197), rigid-invariant
 };
 
-// Row r of Rg from the three angles' sines / cosines: the operations fk_wave_t applies
-// to row r (Rz, then * Ry, then * Rx), zero terms included.
+// Row r of Rg from the three angles' sines / cosines: row r of Rz, then * Ry, then * Rx
+// (fingermodel.cpp:165-180), the products with Rz's constant 0 / 1 entries left out (they
+// only add a signed zero; oracle/hpe_oracle.c rigid_rows forms the same operations).
 __device__ __forceinline__ void rigid_row(int r, double sz, double cz, double sy, double cy,
                                           double sx, double cx, double &g0, double &g1,
                                           double &g2) {
-    double z0, z1, z2;
-    if (r == 0) { z0 = cz; z1 = -sz; z2 = 0; }
-    else if (r == 1) { z0 = sz; z1 = cz; z2 = 0; }
-    else { z0 = 0; z1 = 0; z2 = 1; }
-    const double q0 = z0 * cy + z2 * (-sy);
+    if (r == 2) {  // (0, 0, 1) * Ry * Rx
+        g0 = -sy;
+        g1 = cy * sx;
+        g2 = cy * cx;
+        return;
+    }
+    const double z0 = (r == 0) ? cz : sz, z1 = (r == 0) ? -sz : cz;  // (z0, z1, 0)
+    const double q0 = z0 * cy;
     const double q1 = z1;
-    const double q2 = z0 * sy + z2 * cy;
+    const double q2 = z0 * sy;
     g0 = q0;
     g1 = q1 * cx + q2 * sx;
     g2 = q1 * (-sx) + q2 * cx;
@@ -684,13 +691,20 @@ __device__ __forceinline__ DepthG depth_issue(const FkSm &f, int i, const DevObs
     const int ic = i < HPE_NS ? i : HPE_NS - 1;
     return depth_issue_at(SphXYZ{f.S[ic][0], f.S[ic][1], f.S[ic][2]}, i, o, H);
 }
-__device__ __forceinline__ double depth_finish(DepthG d, const DevObs &o, bool use) {
+// md2p (optional): the off-image value md * md below, computed ahead by the caller with the
+// same operations for the same sphere (the refine: once per call, not per evaluation).
+__device__ __forceinline__ double depth_off_sq(const DevObs &o, double r) {
+    const double md = o.dtmax * o.scale + r;  // off-image: max of the DT (:298)
+    return md * md;
+}
+__device__ __forceinline__ double depth_finish(DepthG d, const DevObs &o, bool use,
+                                               const double *md2p = nullptr) {
     asm volatile("" : "+v"(d.djc), "+v"(d.dtp));
     const double tt = d.djc - d.z;
     const double diff = (0.0 < tt) ? tt : 0.0;  // std::max(0.0, tt)
     const double dd = (double)d.dtp * o.scale + d.r;
-    const double md = o.dtmax * o.scale + d.r;  // off-image: max of the DT (:298)
-    const double v = !d.in ? md * md : (d.djc != 0.0) ? diff * diff : dd * dd;
+    const double md2 = md2p ? *md2p : depth_off_sq(o, d.r);
+    const double v = !d.in ? md2 : (d.djc != 0.0) ? diff * diff : dd * dd;
     return use ? v : 0.0;
 }
 // Block form: wave 0 (its lanes 0..47 are the spheres) issues; the other waves keep a
@@ -1507,18 +1521,23 @@ __device__ __forceinline__ FrozenHead rigid_head(FkSm &f, const DevObs &o,
     r.co = 0.0;
     return r;
 }
-template <class CV>
+// RIGID (hand-frame refine): no collision term (it is the call's constant, added by the
+// caller), and md2p carries the lane's off-image depth value computed once per call.  The
+// lane total al * lambda + dep is >= +0, so leaving out "+ 0.0" changes no bit.
+template <bool RIGID = false, class CV>
 __device__ __forceinline__ double frozen_tail(const FkSm &f, const DevObs &o, const CV &cv,
                                               const DevHand *__restrict__ H,
                                               const int32_t *__restrict__ match,
-                                              FrozenHead hd, const FrozenPts *fp = nullptr) {
+                                              FrozenHead hd, const FrozenPts *fp = nullptr,
+                                              const double *md2p = nullptr) {
     const int l = threadIdx.x & 63;
     double al = fp ? align_frozen_pts(f, *fp, cv, H, l) : align_frozen(f, cv, H, match, l, 64);
     double co = hd.co;
-    asm volatile("" ::"v"(co));  // complete before depth_finish's wait for the gathers
-    const double dep = depth_finish(hd.dg, o, l < HPE_NS);
+    if (!RIGID) asm volatile("" ::"v"(co));  // complete before depth_finish's wait for the gathers
+    const double dep = depth_finish(hd.dg, o, l < HPE_NS, md2p);
     // one wave sum of the lane totals (the three terms' sums in another order: the same
     // value to the last bits, as any order of the reference's own sums)
+    if (RIGID) return wave_sum(al * o.lambda + dep);
     return wave_sum((al * o.lambda + dep) + co);
 }
 template <bool OUTLINE_TRIG = false, class CV>

@@ -1243,7 +1243,8 @@ __device__ __forceinline__ void eval_nodes(RefineSm &rs, int nn, const DevObs &o
                                            const int32_t *__restrict__ match, FkX *Xt,
                                            MwLeader *ml, int *flag, const double *thr = nullptr,
                                            const FrozenPts *fp = nullptr, int rblk = 0,
-                                           const GoldIn *gin = nullptr) {
+                                           const GoldIn *gin = nullptr,
+                                           const double *md2p = nullptr) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     if (!MW) {
         if (w < nn) {
@@ -1255,7 +1256,7 @@ __device__ __forceinline__ void eval_nodes(RefineSm &rs, int nn, const DevObs &o
             } else if (RIGID) {
                 const FrozenHead hd = rblk ? rigid_head<RG_TRANS>(rs.w[w], o, H, rs.rg, *thr)
                                            : rigid_head<RG_ROT>(rs.w[w], o, H, rs.rg, *thr);
-                f = frozen_tail(rs.w[w], o, cv, H, match, hd, fp) + rs.rg.C;
+                f = frozen_tail<true>(rs.w[w], o, cv, H, match, hd, fp, md2p) + rs.rg.C;
             } else {
                 f = eval_wave_frozen<true>(rs.w[w], o, cv, H, match, Xt, thr, fp);
             }
@@ -1486,7 +1487,8 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
                                             double gp, double pl, double gl, int &evals,
                                             double *f_acc, FkX *Xt = nullptr,
                                             MwLeader *ml = nullptr, int *flag = nullptr,
-                                            const FrozenPts *fp = nullptr, int rblk = 0) {
+                                            const FrozenPts *fp = nullptr, int rblk = 0,
+                                            const double *md2p = nullptr) {
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
     StampClock sc;
     sc.start();
@@ -1509,7 +1511,7 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
             if (l < HPE_DOF) rs.w[w].th[l] = thl;
         }
         eval_nodes<MW, RIGID>(rs, nn, o, cv, H, match, Xt, ml, flag, &thl, fp, rblk,
-                              HPE_GOLD_CODED ? &gin : nullptr);
+                              HPE_GOLD_CODED ? &gin : nullptr, md2p);
         if (MW && ml->failed) break;  // the launch is ending early (DevMw::err)
 #if !HPE_GOLD_CODED
         // the serial rules walked level by level on the nodes' costs
@@ -1707,6 +1709,9 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
     // clouds of at most FP_MAX points: each lane keeps its frozen points in registers
     const bool small = !MW && STAGED && o.n >= 1 && o.n <= FP_MAX;  // (N = 0: no point to clamp to)
     FrozenPts fpts;
+    // the lane's sphere (lane l, clamped) off-image depth value, the same for every
+    // evaluation of the call (depth_finish's md * md, computed once)
+    const double md2_l = depth_off_sq(o, H->radii[l < HPE_NS ? l : HPE_NS - 1]);
     for (int blk = 0; blk < 2; ++blk) {
         const int lo = 3 * blk;  // start_idx (PSO.cpp:226-227); end_idx = lo + 2
         // Block 2 moves only the global position u = x0[3..5]: every FK of the block is
@@ -1803,7 +1808,9 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
                 if (RIGID) fk = fk + rs.rg.C;
                 REF_TS(rs.ts_n, 2);
                 if (w < 6) {
-                    double f = frozen_tail(rs.w[w], o, cv, H, match, hd, small ? &fpts : nullptr);
+                    double f = RIGID ? frozen_tail<true>(rs.w[w], o, cv, H, match, hd,
+                                                         small ? &fpts : nullptr, &md2_l)
+                                     : frozen_tail(rs.w[w], o, cv, H, match, hd, small ? &fpts : nullptr);
                     if (RIGID) f = f + rs.rg.C;
                     if (l == 0) rs.fg[w] = f;
                 }
@@ -1837,7 +1844,7 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
             // goldstein(x0, grad, matchId, f_k, optfunc, tk, 30), then x0 = x0 - tk*grad
             const double tk = gold_tree<MW, HPE_GOLD_POLICY, true, RIGID>(
                 rs, o, cv, H, match, fk, gp, pl, gl, evals, nullptr, Xt, &ml, &mwflag,
-                small ? &fpts : nullptr, blk);
+                small ? &fpts : nullptr, blk, &md2_l);
             sc.lap(22);
             if (tk == 0) cnt += 1;
             // tol = sqrt(sum(grad % grad)): arrayops::accumulate (two accumulators)

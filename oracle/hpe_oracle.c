@@ -768,16 +768,18 @@ static void rigid_rows(const double th[3], double G[9]) {
     const double az = deg2rad(th[0] + 180), ay = deg2rad(th[1]), ax = deg2rad(th[2]);
     const double sz = sin(az), cz = cos(az), sy = sin(ay), cy = cos(ay);
     const double sx = sin(ax), cx = cos(ax);
-    for (int r = 0; r < 3; ++r) {
-        double z0, z1, z2;
-        if (r == 0) { z0 = cz; z1 = -sz; z2 = 0; }
-        else if (r == 1) { z0 = sz; z1 = cz; z2 = 0; }
-        else { z0 = 0; z1 = 0; z2 = 1; }
-        const double q0 = z0 * cy + z2 * (-sy), q1 = z1, q2 = z0 * sy + z2 * cy;
+    /* rows of Rz * Ry * Rx without the products with Rz's constant 0 / 1 entries (they only
+     * add a signed zero): the operations of hpe_device.hpp rigid_row */
+    for (int r = 0; r < 2; ++r) {
+        const double z0 = (r == 0) ? cz : sz, z1 = (r == 0) ? -sz : cz;
+        const double q0 = z0 * cy, q1 = z1, q2 = z0 * sy;
         G[3 * r] = q0;
         G[3 * r + 1] = q1 * cx + q2 * sx;
         G[3 * r + 2] = q1 * (-sx) + q2 * cx;
     }
+    G[6] = -sy;
+    G[7] = cy * sx;
+    G[8] = cy * cx;
 }
 
 void ora_rigid_spheres(const ora_hand *h, const double x0[26], const double th[26],
