@@ -258,3 +258,61 @@ def test_raw_sequence_like_pipelined_and_oracle(gh, oracle, ora_hand, np_hand, d
     assert bad(gh.ctx.h, P, 1, sp, None, n, 1, 1, 241.42, 0, None) == hpe._lib.HPE_E_ARG
     assert bad(gh.ctx.h, P, 1, sp, C.c_void_p(d_raw.data_ptr()), n, 1, 1, 241.42, 33, None) == hpe._lib.HPE_E_ARG
     assert bad(gh.ctx.h, P, 1, sp, C.c_void_p(d_raw.data_ptr()), n, 1, 1, 0.0, 0, None) == hpe._lib.HPE_E_ARG
+
+
+def test_raw_sequence_edges(gh, np_hand):
+    """hpe_track_raw_sequence_dev at the edges: one frame (nothing prepared after it),
+    frames_per_graph larger than the sequence, the largest chunk (HPE_SEQ_MAX_CHUNK), and a
+    call after a pipelined sequence (which it ends) -- each equal to the per-frame
+    pipelined loop bit for bit."""
+    import hpe
+    import torch
+    n, P, maxiter = 5, 16, 4
+    poses = hand_data.trajectory(n, seed=31)
+    depth = [oracle_np.render_depth_mm(np_hand, th) for th in poses]
+    ub, lb, sd = oracle_np.reference_bounds()
+    pso = hpe.PSO()
+    pso.set_pso_params(ub, lb, sd, 0.7298, 1.49618, 1.49618, maxiter, 1e-8, 1e-8)
+    pso._push(gh.ctx)
+    rt = gh.ctx.lib
+    st = torch.zeros(27, dtype=torch.float64, device="cuda:0")
+
+    def pipelined(m):
+        st[:26] = torch.from_numpy(oracle_np.X0)
+        st[26] = 0.0
+        torch.cuda.synchronize()
+        gh.ctx.pipeline_begin(depth[0])
+        out = []
+        for f in range(m):
+            gh.ctx.track_pipelined(P, 1, st.data_ptr(), depth[f + 1] if f + 1 < m else None)
+            gh.ctx.check(rt.hpe_sync(gh.ctx.h))
+            out.append(st.cpu().numpy().copy())
+        return np.array(out)
+
+    ref = pipelined(n)
+    d_raw = torch.from_numpy(np.stack(depth).astype(np.float32)).to("cuda:0")
+    hist = torch.empty((n, 27), dtype=torch.float64, device="cuda:0")
+    for m, K in ((1, 0), (1, 8), (n, 32), (n, n + 3)):
+        st[:26] = torch.from_numpy(oracle_np.X0)
+        st[26] = 0.0
+        hist.fill_(float("nan"))
+        torch.cuda.synchronize()
+        gh.ctx.track_raw_sequence(P, 1, st.data_ptr(), d_raw.data_ptr(), m,
+                                  frames_per_graph=K, d_hist_ptr=hist.data_ptr())
+        gh.ctx.check(rt.hpe_sync(gh.ctx.h))
+        h = hist.cpu().numpy()
+        assert np.array_equal(h[:m], ref[:m]), (m, K)
+        assert np.isnan(h[m:]).all(), (m, K)  # rows past the sequence untouched
+    # a pipelined sequence in progress, then a raw sequence: it starts over cleanly
+    st[:26] = torch.from_numpy(oracle_np.X0)
+    torch.cuda.synchronize()
+    gh.ctx.pipeline_begin(depth[0])
+    gh.ctx.track_pipelined(P, 1, st.data_ptr(), depth[1])
+    gh.ctx.check(rt.hpe_sync(gh.ctx.h))
+    st[:26] = torch.from_numpy(oracle_np.X0)
+    st[26] = 0.0
+    torch.cuda.synchronize()
+    gh.ctx.track_raw_sequence(P, 1, st.data_ptr(), d_raw.data_ptr(), n, frames_per_graph=2,
+                              d_hist_ptr=hist.data_ptr())
+    gh.ctx.check(rt.hpe_sync(gh.ctx.h))
+    assert np.array_equal(hist.cpu().numpy(), ref)
