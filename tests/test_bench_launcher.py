@@ -40,3 +40,30 @@ def test_self_launch_two_ranks_stub():
 def test_single_rank_stub():
     r = _bench("--stub", "--steps", "2", "--warmup", "0")
     assert r["n_gpus"] == 1 and r["winner_rank"] == 0
+
+
+def test_frames_per_graph_defaults(monkeypatch):
+    """The frame loop bench.py times: on one GPU the raw frames resident in HBM, 8 frames per
+    graph (hpe_track_raw_sequence_dev); with N > 1, --dump or a per-generation exchange, one
+    graph per frame (the exchange / dump sit between frames); an explicit value wins where
+    allowed and is refused where a step sits between frames."""
+    import importlib
+    import pytest
+    sys.path.insert(0, str(hand_data.ROOT))
+    bench = importlib.import_module("bench")
+
+    def parse(*argv):
+        monkeypatch.setattr(sys, "argv", ["bench.py", *argv])
+        return bench.parse()
+
+    assert parse().frames_per_graph == 8
+    assert parse("--resident").frames_per_graph == 8
+    assert parse("--gpus", "2").frames_per_graph == 0
+    assert parse("--dump", "/tmp/x").frames_per_graph == 0
+    assert parse("--exchange", "gen:5").frames_per_graph == 0
+    assert parse("--frames-per-graph", "0").frames_per_graph == 0
+    assert parse("--frames-per-graph", "4").frames_per_graph == 4
+    for bad in (("--gpus", "2", "--frames-per-graph", "8"),
+                ("--exchange", "gen:5", "--frames-per-graph", "8")):
+        with pytest.raises(SystemExit):
+            parse(*bad)
