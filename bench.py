@@ -460,7 +460,7 @@ def main():
                 if ex is not None:
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record(ext)
-                exchange_best(state, gathered)
+                exchange_best(state, gathered, ctx=ctx)  # all-gather + hpe_pick_best
                 if ex is not None:
                     e1.record(ext)
                     ex.append((e0, e1))

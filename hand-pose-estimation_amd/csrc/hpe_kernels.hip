@@ -792,6 +792,33 @@ __global__ __launch_bounds__(HPE_NT) void k_swarm_best(DevSwarm sw, int g) {
     if (t == HPE_DOF) sw.ext[HPE_DOF] = sw.pch[(size_t)g * P + b.i];
 }
 
+// Multi-GPU subswarms, the per-frame best of N (hpe_pick_best): state <- the
+// row of gathered (world x 27: {bestp, cost} per rank) with the smallest cost, in one launch
+// on the tracker stream right after the all-gather.  Exactly hpe/dist.py pick_best
+// (torch.nan_to_num(cost, nan=inf) then the first argmin): NaN -> +inf, +inf -> the largest
+// finite double, -inf -> the lowest; ties go to the lowest rank.  One wave, world <= 64.
+__global__ __launch_bounds__(64) void k_pick_best(const double *__restrict__ gathered, int world,
+                                                  double *__restrict__ state) {
+    __shared__ double cost[64];
+    __shared__ int win;
+    const int l = threadIdx.x;
+    double v = (l < world) ? gathered[(size_t)l * (HPE_DOF + 1) + HPE_DOF] : 0.0;
+    if (v != v) v = __builtin_inf();
+    else if (v == __builtin_inf()) v = 1.7976931348623157e308;
+    else if (v == -__builtin_inf()) v = -1.7976931348623157e308;
+    cost[l] = v;
+    wave_sync();
+    if (l == 0) {
+        int w = 0;
+        for (int r = 1; r < world; ++r)
+            if (cost[r] < cost[w]) w = r;
+        win = w;
+    }
+    wave_sync();
+    const int w = win;
+    if (l <= HPE_DOF) state[l] = gathered[(size_t)w * (HPE_DOF + 1) + l];
+}
+
 // u64 wave helpers of k_pso_final's replay: lane l - 1's value (lane 0: fill), the
 // inclusive prefix minimum over lanes 0..l (DPP row_shr 1/2/4/8, row_bcast 15/31; lanes
 // without a source keep the identity, all ones), a lane's value in every lane.

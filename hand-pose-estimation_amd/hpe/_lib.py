@@ -69,6 +69,7 @@ SIGNATURES = {
     "hpe_set_refine_exact": (C.c_int, [C.c_void_p, C.c_int]),
     "hpe_graph_captures": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
     "hpe_set_exchange": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "hpe_pick_best": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),
     "hpe_get_refine_exact": (C.c_int, [C.c_void_p]),
     "hpe_track_frame": (C.c_int, [C.c_void_p, C.c_int, C.c_int, dp, dp]),
     "hpe_track_frame_dev": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),

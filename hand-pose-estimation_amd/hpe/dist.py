@@ -34,16 +34,23 @@ def pick_best(gathered: torch.Tensor) -> torch.Tensor:
 
 
 def exchange_best(state: torch.Tensor, gathered: torch.Tensor | None = None,
-                  group=None) -> torch.Tensor:
+                  group=None, ctx=None) -> torch.Tensor:
     """In place: state <- best state over all ranks.  Runs on the current stream (the
-    caller wraps it in the tracker's stream so no host synchronisation is needed)."""
+    caller wraps it in the tracker's stream so no host synchronisation is needed).
+    ctx (a device state and the tracker context whose stream is current): the pick is
+    hpe_pick_best, one launch on that stream, instead of pick_best's torch kernels."""
     world = dist.get_world_size(group)
     if world == 1:
         return state
     if gathered is None:
         gathered = state.new_empty(world * STATE_LEN)
     dist.all_gather_into_tensor(gathered, state, group=group)
-    state.copy_(pick_best(gathered.view(world, STATE_LEN)))
+    if ctx is not None and state.is_cuda:
+        import ctypes as C
+        ctx.check(ctx.lib.hpe_pick_best(ctx.h, C.c_void_p(gathered.data_ptr()), world,
+                                        C.c_void_p(state.data_ptr())))
+    else:
+        state.copy_(pick_best(gathered.view(world, STATE_LEN)))
     return state
 
 

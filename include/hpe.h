@@ -150,6 +150,13 @@ int hpe_set_seed(hpe_ctx *ctx, uint64_t seed);
 int hpe_pso_evolve(hpe_ctx *ctx, const double x0[26], int num_p, double bestp[26],
                    double *bestcost_out);
 
+/* Multi-GPU subswarms, the per-frame best of N after the caller's all-gather
+ * of every rank's 27-double state: d_state <- the row of d_gathered (world x 27 device
+ * doubles, {bestp, cost} per rank) with the smallest cost -- NaN never wins, ties go to the
+ * lowest rank (hpe/dist.py pick_best) -- as one launch on hpe_stream(ctx).  world 1..64.
+ * Replaces the reference's shared gbest across its OpenMP loop (PSO.cpp:848-861). */
+int hpe_pick_best(hpe_ctx *ctx, const double *d_gathered, int world, double *d_state);
+
 /* Opt-in per-generation exchange between subswarms (ICP-PSO style; NOT the reference's
  * algorithm, whose gbest never enters the velocity, PSO.cpp:824-832).  every > 0: after
  * every `every`-th generation g < maxiter-1 of each pso_evolve of this context (standalone

@@ -68,3 +68,49 @@ def test_rccl_one_rank_allgather_on_tracker_stream(tmp_path):
     assert out.returncode == 0, out.stderr[-3000:]
     assert "RCCL" in out.stdout and "backend nccl" in out.stdout, out.stdout
     print(out.stdout.strip())
+
+
+def test_pick_best_kernel_equals_torch_pick_best():
+    """hpe_pick_best (the per-frame best of N in one launch, used after the RCCL all-gather)
+    against hpe.dist.pick_best on the same gathered rows: random costs, equal costs (lowest
+    rank wins), NaN costs (never win), +inf / -inf costs, world 1 .. 64."""
+    import ctypes as C
+
+    import numpy as np
+    import torch
+
+    import hpe
+    from hpe.dist import pick_best
+    hand = hpe.reference_hand(device=0)
+    ctx = hand.ctx
+    rng = np.random.default_rng(5)
+    for world in (1, 2, 3, 8, 64):
+        for case in range(6):
+            g = rng.normal(size=(world, 27))
+            c = rng.uniform(1, 10, size=world)
+            if case == 1:
+                c[:] = 4.0
+            elif case == 2:
+                c[rng.integers(world)] = np.nan
+            elif case == 3:
+                c[:] = np.nan
+            elif case == 4:
+                c[rng.integers(world)] = np.inf
+                c[rng.integers(world)] = np.nan
+            elif case == 5:
+                c[rng.integers(world)] = -np.inf
+            g[:, 26] = c
+            gt = torch.from_numpy(g.ravel().copy()).to("cuda:0")
+            st = torch.zeros(27, dtype=torch.float64, device="cuda:0")
+            torch.cuda.synchronize()
+            ctx.check(ctx.lib.hpe_pick_best(ctx.h, C.c_void_p(gt.data_ptr()), world,
+                                            C.c_void_p(st.data_ptr())))
+            ctx.check(ctx.lib.hpe_sync(ctx.h))
+            want = pick_best(torch.from_numpy(g.copy())).numpy()
+            got = st.cpu().numpy()
+            assert np.array_equal(got, want, equal_nan=True), (world, case)
+    assert ctx.lib.hpe_pick_best(ctx.h, None, 2, None) == hpe._lib.HPE_E_ARG
+    gt = torch.zeros(27 * 65, dtype=torch.float64, device="cuda:0")
+    assert ctx.lib.hpe_pick_best(ctx.h, C.c_void_p(gt.data_ptr()), 65,
+                                 C.c_void_p(gt.data_ptr())) == hpe._lib.HPE_E_ARG
+    ctx.close()
