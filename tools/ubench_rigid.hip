@@ -2,7 +2,8 @@
 // (hpe_device.hpp rigid_wave / rigid_head / frozen_tail), not part of the product.
 // One workgroup; NW waves (argv[1], default 1) each evaluate nodes concurrently, wave 0
 // times them with s_memtime: the latency of each piece alone and with 2 waves per SIMD.
-// Build: hipcc -O3 -std=c++17 -ffp-contract=off --offload-arch=gfx950 tools/ubench_rigid.hip
+// Build: hipcc -O3 -std=c++17 -ffp-contract=off --offload-arch=gfx950 -o tools/ubench_rigid \
+//        tools/ubench_rigid.hip hand-pose-estimation_amd/csrc/hpe_host.cpp
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
