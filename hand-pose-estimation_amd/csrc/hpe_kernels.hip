@@ -1145,6 +1145,12 @@ __device__ __forceinline__ void gold_down(double a, double &b, double &alpha) {
 #ifndef HPE_GOLD_CODED
 #define HPE_GOLD_CODED 0
 #endif
+#ifndef HPE_RF_SPREAD
+#define HPE_RF_SPREAD 1
+#endif
+#ifndef HPE_RF_HEAD_FIRST
+#define HPE_RF_HEAD_FIRST 0
+#endif
 #ifndef HPE_RIGID_FUSED
 #define HPE_RIGID_FUSED 0
 #endif
@@ -1796,16 +1802,36 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
                 // them: the search stores matchId, and while the slowest search waves and the
                 // corr sums finish, waves 0..5 already run the parts of their gradient point
                 // that need no matchId (FK, depth gathers, collision)
+                FrozenHead hd{};
+                auto head = [&]() {
+                    if (w < 6) {
+                        const int d = lo + (w >> 1);
+                        const double xl = rs.x0[l < HPE_DOF ? l : 0];
+                        const double thl = (l == d) ? ((w & 1) ? xl - e : xl + e) : xl;
+                        if (l < HPE_DOF) rs.w[w].th[l] = thl;
+                        wave_sync();
+                        if (RIGID) hd = blk ? rigid_head<RG_TRANS>(rs.w[w], o, H, rs.rg, thl)
+                                            : rigid_head<RG_ROT>(rs.w[w], o, H, rs.rg, thl);
+                        else hd = frozen_head<true>(rs.w[w], o, H, Xt, &thl);
+                    }
+                };
+                // HPE_RF_HEAD_FIRST (hand-frame form): the head before the search, so its
+                // depth gathers are in flight during the search
+                constexpr bool head_first = RIGID && HPE_RF_HEAD_FIRST;
+                if (head_first) head();
                 const DepthG dgc = depth_issue_w0(rs.base, o, H);
                 const bool young = w >= HPE_SETPRIO_FROM;  // as in eval_block
                 if (young) __builtin_amdgcn_s_setprio(1);
-                // (n <= 256) the items go where the SIMDs have room: waves 0..5 also run a
-                // gradient point's head below, two of them on SIMDs 0 and 1 each, one on
-                // SIMDs 2 and 3; so waves 4, 5 search nothing and waves 6, 7 two items
+                // (n <= 256) the items go where the SIMDs have room.  Chain form: waves 0..5
+                // also run a gradient point's head below (FK), two of them on SIMDs 0 and 1
+                // each, one on SIMDs 2 and 3; so waves 4, 5 search nothing and waves 6, 7 two
+                // items.  Hand-frame form (HPE_RF_SPREAD): the heads are short (no DH chain),
+                // so every wave takes one item and no wave searches twice.
                 double al;
                 if (small) {
-                    const int f0 = (w < 4) ? 64 * w : (w >= 6) ? 256 + 128 * (w - 6) : 0;
-                    const int cnt = (w < 4) ? 1 : (w >= 6) ? 2 : 0;
+                    const bool spread = RIGID && HPE_RF_SPREAD;
+                    const int f0 = (w < 4 || spread) ? 64 * w : (w >= 6) ? 256 + 128 * (w - 6) : 0;
+                    const int cnt = (w < 4 || spread) ? 1 : (w >= 6) ? 2 : 0;
                     al = search_align<RF_NT, true>(rs.base, cv, H, match, load_pt(cv, f0 + l),
                                                    f0 + l, BT_GENS, 64, cnt);
                 } else {
@@ -1816,17 +1842,7 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
                 const double dep = depth_finish(dgc, o, t < HPE_NS);
                 const double tot = wave_sum((al * o.lambda + dep) + co);  // as block_sum1
                 if (l == 0) rs.red[w][0] = tot;
-                FrozenHead hd{};
-                if (w < 6) {
-                    const int d = lo + (w >> 1);
-                    const double xl = rs.x0[l < HPE_DOF ? l : 0];
-                    const double thl = (l == d) ? ((w & 1) ? xl - e : xl + e) : xl;
-                    if (l < HPE_DOF) rs.w[w].th[l] = thl;
-                    wave_sync();
-                    if (RIGID) hd = blk ? rigid_head<RG_TRANS>(rs.w[w], o, H, rs.rg, thl)
-                                        : rigid_head<RG_ROT>(rs.w[w], o, H, rs.rg, thl);
-                    else hd = frozen_head<true>(rs.w[w], o, H, Xt, &thl);
-                }
+                if (!head_first) head();
                 __syncthreads();  // matchId complete, the corr partial sums in red
                 if (small) load_frozen_pts(fpts, cv, match, l);
                 fk = 0;
