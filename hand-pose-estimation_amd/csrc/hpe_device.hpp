@@ -675,13 +675,8 @@ __device__ __forceinline__ DepthG depth_issue_at(const SphXYZ &c, int i, const D
     DepthG d;
     d.in = dx >= 0 && dx < HPE_IMG_W && dy >= 0 && dy < HPE_IMG_H;  // NaN: off-image
     const int pix = d.in ? (int)dy * HPE_IMG_W + (int)dx : 0;
-#ifdef HPE_DIAG_NO_GATHER  // diagnostic timing build only: results invalid
-    d.djc = (double)(pix & 7);
-    d.dtp = (float)(pix & 3);
-#else
     d.djc = gp(o.depth)[pix];
     d.dtp = gp(o.dt)[pix];
-#endif
     d.z = z;
     d.r = H->radii[i];
     return d;
@@ -870,188 +865,11 @@ struct Pt {
     double x, y, z;
 };
 
-// ---------------------------------------------------------------- MFMA-filtered search
-// HPE_MFMA_SEARCH=1: the 48 squared distances of 32 points come from two
-// v_mfma_f32_32x32x16_f16 (spheres x points) as an approximation e^ of
-//     t = |p' - c'|^2 + BIAS = |p'|^2 + |c'|^2 - 2 p'.c' + BIAS
-// in coordinates centred on sphere 0 (p' = fl(q - o), c' = fl(c - o), fp32), every fp32
-// value split into two fp16 (hi + lo), p'.c' as ph.ch + ph.cl + pl.ch (pl.cl dropped).  Each
-// lane keeps the smallest and second smallest key (bits(e^) with the sphere index in the low
-// 6 bits) of its 24 spheres; the lane pair (l, l ^ 32) holds a point's 48.  When the second
-// smallest exceeds the smallest by more than M (below), no other sphere can come within the
-// sqrt class of BFMatcher's minimum, so the smallest IS the match bf_search returns; any
-// other point (a near tie, a non-finite point, coordinates beyond 250 cm) sends its wave's
-// 32 points through bf_search itself.  The matches are bf_search's, bit for bit.
-// Bound (P >= |p'|, C >= |c'|, S = P + C, u = 2^-24): |e^ - t| <= E = 30 u S^2 + 3.6 2^-14 S
-// + 14 u, from the fp32 roundings of p', c', |p'|^2, |c'|^2 (<= 3.1 u each), the hi / lo
-// residuals (<= 2^-22 relative, or 2^-14 absolute if the unit flushes fp16 subnormals), the
-// dropped pl.cl (<= 2^-22 P C) and at most 13 fp32 roundings of the accumulation
-// (<= 13 u sum|terms|, sum|terms| <= 1.01 S^2 + BIAS); the centring moves d^2 by
-// <= 3.6 u S^2; BFMatcher's fp32 d^2 is within 5 u d^2 of the real one and its sqrt class
-// within 8 u; the keys truncate e^ by < 2^-17 e^.  A sphere j != j1 is then outside the
-// class whenever e^_j - v1 > 2.02 E + 2^-16 v1, so
-//     M = 2^-18 S^2 + 2^-11 S + 2^-16 v1 + 2^-17 + 2^-20 v2   (>= that, fp32-evaluated).
-#ifndef HPE_MFMA_SEARCH
-#define HPE_MFMA_SEARCH 0
-#endif
-typedef _Float16 hpe_h8 __attribute__((ext_vector_type(8)));
-typedef float hpe_f16x __attribute__((ext_vector_type(16)));
-#define MF_BIAS 1.0f
-// the allowance for fp16 subnormals flushed by the unit (3.6 2^-14 per cm of S)
-#ifndef MF_FLUSH
-#define MF_FLUSH 0x1p-11f
-#endif
-struct MfmaSph {
-    hpe_h8 a0, a1;     // sphere fragments: tile 0 = spheres 0..31, tile 1 = 32..47 (+ zero rows)
-    float ox, oy, oz;  // the origin: sphere 0's fp32 centre
-    float C;           // >= |c'| over the 48 spheres
-};
-__device__ __forceinline__ void mf_split(float v, _Float16 &hi, _Float16 &lo) {
-    hi = (_Float16)v;
-    lo = (_Float16)(v - (float)hi);  // exact in fp32: v's bits below hi
-}
-__device__ __forceinline__ unsigned mf_xor32_u(unsigned v) { return (unsigned)__shfl_xor((int)v, 32); }
-// the middle of three (v_med3_u32)
-__device__ __forceinline__ unsigned umed3(unsigned a, unsigned b, unsigned c) {
-    return max(min(a, b), min(max(a, b), c));
-}
-// The wave's sphere fragments from f.Sp (every lane of the wave calls it).
-__device__ __forceinline__ MfmaSph mfma_sph(const FkSm &f) {
-    const int l = threadIdx.x & 63, r = l & 31, h = l >> 5;
-    MfmaSph m;
-    m.ox = f.Sp[0][0];
-    m.oy = f.Sp[1][0];
-    m.oz = f.Sp[2][0];
-    float cn = 0.f;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        const int s = 32 * t + r;
-        const bool ok = s < HPE_NS;
-        const int sc = ok ? s : 0;
-        const float cx = f.Sp[0][sc] - m.ox, cy = f.Sp[1][sc] - m.oy, cz = f.Sp[2][sc] - m.oz;
-        const float cc = (cx * cx + cy * cy) + cz * cz;
-        _Float16 hx, lx, hy, ly, hz, lz, hc, lc;
-        mf_split(cx, hx, lx);
-        mf_split(cy, hy, ly);
-        mf_split(cz, hz, lz);
-        mf_split(cc, hc, lc);
-        const _Float16 one = ok ? (_Float16)1.0f : (_Float16)0.0f, z = (_Float16)0.0f;
-        hpe_h8 a;
-        if (h == 0) {
-            a = hpe_h8{hx, hy, hz, lx, ly, lz, hx, hy};
-        } else {
-            a = hpe_h8{hz, hc, lc, one, one, one, z, z};
-        }
-        if (!ok) a = hpe_h8{z, z, z, z, z, z, z, z};
-        if (t == 0) m.a0 = a;
-        else m.a1 = a;
-        cn = fmaxf(cn, ok ? cc : 0.f);
-    }
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) cn = fmaxf(cn, __shfl_xor(cn, o));
-    m.C = sqrtf(cn) * 1.000001f;
-    return m;
-}
-// One tile of 32 points (column r of the wave; both halves of a lane pair load the same
-// point): the match of point r (bf_search's, both lanes of the pair get it).  q*: the
-// point's fp32 coordinates.  Returns -1 where bf_search must decide (the caller sends the
-// wave's tile there, wave-uniformly).
-__device__ __forceinline__ int mfma_match(const FkSm &f, const MfmaSph &m, float qx, float qy,
-                                          float qz) {
-    const int l = threadIdx.x & 63, h = l >> 5;
-    const float px = qx - m.ox, py = qy - m.oy, pz = qz - m.oz;
-    const float pp = (px * px + py * py) + pz * pz;
-    _Float16 hx, lx, hy, ly, hz, lz, hp, lp;
-    mf_split(px, hx, lx);
-    mf_split(py, hy, ly);
-    mf_split(pz, hz, lz);
-    mf_split(pp, hp, lp);
-    const _Float16 m2 = (_Float16)-2.0f, one = (_Float16)1.0f, z = (_Float16)0.0f;
-    hpe_h8 b;
-    if (h == 0) {
-        b = hpe_h8{m2 * hx, m2 * hy, m2 * hz, m2 * hx, m2 * hy, m2 * hz, m2 * lx, m2 * ly};
-    } else {
-        b = hpe_h8{m2 * lz, one, one, hp, lp, (_Float16)MF_BIAS, z, z};
-    }
-    const hpe_f16x zero = {};
-    const hpe_f16x e0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(m.a0, b, zero, 0, 0, 0);
-    const hpe_f16x e1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(m.a1, b, zero, 0, 0, 0);
-    // keys: row (sphere) of register k = (k & 3) + 8 (k >> 2) + 4 h; 4 h is added after
-    // the lane's reduction (it orders none of the lane's own keys)
-    unsigned key[24];
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-        key[k] = (__float_as_uint(e0[k]) & 0xFFFFFFC0u) | (unsigned)((k & 3) + 8 * (k >> 2));
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-        key[16 + k] = (__float_as_uint(e1[k]) & 0xFFFFFFC0u) | (unsigned)(32 + (k & 3) + 8 * (k >> 2));
-    // smallest / second smallest: triples (min3, med3), then three-way merges
-    unsigned a1[8], a2[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        a1[k] = min(min(key[3 * k], key[3 * k + 1]), key[3 * k + 2]);
-        a2[k] = umed3(key[3 * k], key[3 * k + 1], key[3 * k + 2]);
-    }
-    auto merge3 = [](unsigned x1, unsigned x2, unsigned y1, unsigned y2, unsigned z1, unsigned z2,
-                     unsigned &o1, unsigned &o2) {
-        o1 = min(min(x1, y1), z1);
-        o2 = min(umed3(x1, y1, z1), min(min(x2, y2), z2));
-    };
-    unsigned b1, b2, c1, c2, d1, d2, M1, M2;
-    merge3(a1[0], a2[0], a1[1], a2[1], a1[2], a2[2], b1, b2);
-    merge3(a1[3], a2[3], a1[4], a2[4], a1[5], a2[5], c1, c2);
-    d1 = min(a1[6], a1[7]);
-    d2 = umed3(a1[6], a1[7], min(a2[6], a2[7]));
-    merge3(b1, b2, c1, c2, d1, d2, M1, M2);
-    M1 += 4u * (unsigned)h;
-    M2 += 4u * (unsigned)h;
-    const unsigned P1 = mf_xor32_u(M1), P2 = mf_xor32_u(M2);
-    const unsigned F1 = min(M1, P1), F2 = umed3(M1, P1, min(M2, P2));
-    const float v1 = __uint_as_float(F1 & 0xFFFFFFC0u), v2 = __uint_as_float(F2 & 0xFFFFFFC0u);
-    const float S = sqrtf(pp) * 1.000001f + m.C;
-    const float Mb = ((0x1p-18f * S) * S + MF_FLUSH * S) + (0x1p-16f * v1 + 0x1p-17f);
-    const bool fin = (S < 250.f) && v1 > 0.f;  // false for NaN
-    const bool single = fin && (v2 - v1 > Mb + 0x1p-20f * v2);
-    if (!__ballot(!single)) return (int)(F1 & 63u);  // the common case: every point decided
-    // a point of this wave has a second sphere within M: if the third smallest is clear of
-    // M, the two smallest are the only candidates and their fp32 d^2 (bf_search's
-    // operations) decide -- BFMatcher's match is the first candidate within the sqrt class
-    // of their minimum.  Three or more candidates: -1 (bf_search).
-    asm volatile("" ::: "memory");  // keeps this rare path's work out of the common one
-    unsigned t3 = ~0u;
-#pragma unroll
-    for (int k = 0; k < 24; ++k) {
-        const unsigned kg = key[k] + 4u * (unsigned)h;
-        t3 = min(t3, kg > F2 ? kg : ~0u);
-    }
-    const unsigned T3 = min(t3, mf_xor32_u(t3));
-    const float v3 = __uint_as_float(T3 & 0xFFFFFFC0u);
-    const bool pair = fin && !single && (v3 - v1 > Mb + 0x1p-20f * v3);
-    int idx = single ? (int)(F1 & 63u) : -1;
-    if (pair) {
-        const int j1 = (int)(F1 & 63u), j2 = (int)(F2 & 63u);
-        const float t1x = qx - f.Sp[0][j1], t1y = qy - f.Sp[1][j1], t1z = qz - f.Sp[2][j1];
-        const float t2x = qx - f.Sp[0][j2], t2y = qy - f.Sp[1][j2], t2z = qz - f.Sp[2][j2];
-        const float D1 = (t1x * t1x + t1y * t1y) + t1z * t1z;
-        const float D2 = (t2x * t2x + t2y * t2y) + t2z * t2z;
-        const float hi = hi_sqrt_class(fminf(D1, D2));
-        const int a = min(j1, j2), b = max(j1, j2);
-        idx = ((a == j1 ? D1 : D2) <= hi) ? a : b;
-    }
-    return idx;
-}
 template <class CV>
 __device__ __forceinline__ Pt load_pt(const CV &cv, int it) {
-#if HPE_MFMA_SEARCH
-    // the point of lane (it & 31) in the first tile (it / 64) of the MFMA layout, clamped
-    const int p = min(32 * (it >> 6) + (it & 31), cv.n - 1);
-    if (p >= 0) return Pt{cv.cx[p], cv.cy[p], cv.cz[p]};
-    return Pt{0, 0, 0};
-#else
     const int p = it >> 1;
     if (it < 2 * cv.n) return Pt{cv.cx[p], cv.cy[p], cv.cz[p]};
     return Pt{0, 0, 0};
-#endif
 }
 // pre: the point of item threadIdx.x, loaded early by the caller (load_pt) so its
 // latency hides under FK.
@@ -1066,50 +884,6 @@ __device__ __forceinline__ double search_align(const FkSm &f, const CV &cv,
                                                int stride = NT, int max_items = 1 << 30) {
     if (gt < 0) gt = threadIdx.x;
     double acc = 0.0;
-#if HPE_MFMA_SEARCH
-    {
-        // tiles of 32 points: this wave's first is gt / 64, then every stride / 64-th
-        // (the item layout's points gt/2, gt/2 + stride/2, ... are the same wave's tiles), at
-        // most max_items of them.  Lane (r, h): point r of the tile, spheres of half h.
-        if (32 * (gt >> 6) >= cv.n || max_items <= 0) return 0.0;
-        const int l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
-        const int tstride = stride >> 6;
-        const MfmaSph ms = mfma_sph(f);
-        int k = 0;
-        // the first tile's point is pre (load_pt(cv, gt), loaded by the caller ahead); each
-        // later one is loaded a tile ahead (clamped, unconditional)
-        double X = pre.x, Y = pre.y, Z = pre.z;
-        for (int tile = gt >> 6; 32 * tile < cv.n && k < max_items; tile += tstride, ++k) {
-            const int p = 32 * tile + r;
-            const int pn = min(p + 32 * tstride, cv.n - 1);
-            const double Xn = cv.cx[pn], Yn = cv.cy[pn], Zn = cv.cz[pn];
-            const float qx = (float)X, qy = (float)Y, qz = (float)Z;
-            int idx = mfma_match(f, ms, qx, qy, qz);
-            if (__ballot(idx < 0)) {
-                asm volatile("" ::: "memory");  // (none of this ahead of the branch)
-                // bf_search for the wave's 32 points in its own layout (lanes 2j, 2j + 1:
-                // point j, sphere halves 0 / 1), the result moved to lane j (and j + 32)
-                const int h2 = l & 1, pj = min(32 * tile + (l >> 1), cv.n - 1);
-                const float bx = (float)cv.cx[pj], by = (float)cv.cy[pj], bz = (float)cv.cz[pj];
-                const BfOut rb = bf_search(f, H, f.Sp[0] + 24 * h2, f.Sp[1] + 24 * h2,
-                                           f.Sp[2] + 24 * h2, bx, by, bz, h2, g_ts);
-                idx = __shfl(rb.idx, 2 * r);
-            }
-            const int ic = idx < HPE_NS ? idx : 0;  // >= 48: all-NaN point (reference undefined)
-            if (hh == 0 && p < cv.n) {
-                const double cx = f.S[ic][0], cy = f.S[ic][1], cz = f.S[ic][2], cr = H->radii[ic];
-                const double dx = X - cx, dy = Y - cy, dz = Z - cz;
-                const double e = sqrt((dx * dx + dy * dy) + dz * dz) - cr;
-                acc += e * e;
-                if (STORE_MATCH) match[p] = ic;
-            }
-            X = Xn;
-            Y = Yn;
-            Z = Zn;
-        }
-        return acc;
-    }
-#endif
     const int h = gt & 1;
     const float *SX = f.Sp[0] + 24 * h, *SY = f.Sp[1] + 24 * h, *SZ = f.Sp[2] + 24 * h;
     BLK_TS(g_ts, 15);
@@ -1411,103 +1185,6 @@ __device__ __forceinline__ FrozenHead frozen_head(FkSm &f, const DevObs &o,
            ((l < 16) ? collide_value(cp[2], rt[2]) : 0.0);
     return r;
 }
-// A whole Goldstein node of the rigid refine on one wave, for clouds of at most FP_MAX
-// points (the lane's matchIds in fp): the rotation rows are formed once, then the lane's own
-// sphere (stored for the accepted-node copy, projected for the depth term) and its four
-// points' matched centres are placed straight from the hand frame in registers -- the
-// same operations as rigid_wave, so the same bits -- with no LDS round trip between the
-// placement and the alignment.  All hand-frame / point reads are issued before the trig.
-// Returns cal_cost2(theta, matchId, false) = sum(align * lambda + depth) + R.C.
-template <int MODE, bool OUTLINE_TRIG = HPE_RIGID_OUTLINE_TRIG, class CV>
-__device__ __forceinline__ double rigid_node(FkSm &f, const DevObs &o, const CV &cv,
-                                             const DevHand *__restrict__ H, const RigidSm &R,
-                                             double thl, const FrozenPts &fp) {
-    const int l = threadIdx.x & 63;
-    const int sl = l < HPE_NS ? l : HPE_NS - 1;
-    const bool tr = MODE == RG_TRANS;
-    const double a0 = tr ? R.P[sl][0] : R.q[sl][0];
-    const double a1 = tr ? R.P[sl][1] : R.q[sl][1];
-    const double a2 = tr ? R.P[sl][2] : R.q[sl][2];
-    const double rr = H->radii[sl];
-    double px[4], py[4], pz[4], bx[4], by[4], bz[4], sr[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int q = min(l + 64 * k, cv.n - 1), id = fp.id[k];
-        px[k] = cv.cx[q];
-        py[k] = cv.cy[q];
-        pz[k] = cv.cz[q];
-        bx[k] = tr ? R.P[id][0] : R.q[id][0];
-        by[k] = tr ? R.P[id][1] : R.q[id][1];
-        bz[k] = tr ? R.P[id][2] : R.q[id][2];
-        sr[k] = H->radii[id];
-    }
-    const double u0 = readlane_f64(thl, 3), u1 = readlane_f64(thl, 4), u2 = readlane_f64(thl, 5);
-    double g[9];
-    if (!tr) {
-        double s = 0.0, c = 1.0;
-        if (l < 3) {  // TWS, ANG, ROT (fingermodel.cpp:91-93)
-            const double a = deg2rad(l == 0 ? thl + 180 : thl);
-            if (OUTLINE_TRIG) {
-                const SinCos r = sincos_outline(a);
-                s = r.s;
-                c = r.c;
-            } else {
-                sincos(a, &s, &c);
-            }
-        }
-        const double sz = readlane_f64(s, 0), cz = readlane_f64(c, 0);
-        const double sy = readlane_f64(s, 1), cy = readlane_f64(c, 1);
-        const double sx = readlane_f64(s, 2), cx = readlane_f64(c, 2);
-#pragma unroll
-        for (int r = 0; r < 3; ++r) rigid_row(r, sz, cz, sy, cy, sx, cx, g[3 * r], g[3 * r + 1], g[3 * r + 2]);
-    }
-    // coordinate r of a centre from its hand-frame (or, translation block, rotated) row
-    auto place = [&](double b0, double b1, double b2, int r, double u) {
-        const double p = tr ? (r == 0 ? b0 : r == 1 ? b1 : b2)
-                            : (g[3 * r] * b0 + g[3 * r + 1] * b1) + g[3 * r + 2] * b2;
-        return p + u;
-    };
-    // the lane's own sphere: stored (read after the round's barrier if this node is
-    // accepted) and projected
-    const double v0 = place(a0, a1, a2, 0, u0);
-    const double v1 = place(a0, a1, a2, 1, u1) * -1;  // handmodel.cpp:288
-    const double v2 = place(a0, a1, a2, 2, u2) * -1;
-    if (l < HPE_NS) {
-        f.S[l][0] = v0;
-        f.S[l][1] = v1;
-        f.S[l][2] = v2;
-        f.Sp[0][l] = (float)v0;
-        f.Sp[1][l] = (float)v1;
-        f.Sp[2][l] = (float)v2;
-    }
-    DepthG dg = depth_issue_at(SphXYZ{v0, v1, v2}, l, o, H);
-    dg.r = rr;
-    // the frozen alignment (align_frozen_pts' per-point operations)
-    double d2[4], rt[4], e[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const double sx0 = place(bx[k], by[k], bz[k], 0, u0);
-        const double sy0 = place(bx[k], by[k], bz[k], 1, u1) * -1;
-        const double sz0 = place(bx[k], by[k], bz[k], 2, u2) * -1;
-        const double dx = px[k] - sx0, dy = py[k] - sy0, dz = pz[k] - sz0;
-        d2[k] = (dx * dx + dy * dy) + dz * dz;
-        rt[k] = hpe_sqrt_nr(d2[k]);
-    }
-    if (!(hpe_sqrt_direct(d2[0]) && hpe_sqrt_direct(d2[1]) && hpe_sqrt_direct(d2[2]) &&
-          hpe_sqrt_direct(d2[3]))) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) rt[k] = hpe_sqrt_direct(d2[k]) ? rt[k] : sqrt(d2[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const double r = rt[k] - sr[k];
-        e[k] = (l + 64 * k < cv.n) ? r * r : 0.0;
-    }
-    const double al = (e[0] + e[1]) + (e[2] + e[3]);
-    const double dep = depth_finish(dg, o, l < HPE_NS);
-    return wave_sum((al * o.lambda + dep) + 0.0) + R.C;
-}
-
 // frozen_head of the rigid refine (rigid_wave above): the collision is the constant R.C,
 // added by the caller after the sum.
 template <int MODE>

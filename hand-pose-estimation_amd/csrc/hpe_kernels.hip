@@ -861,7 +861,7 @@ __device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v,
 // the block evaluates it.
 template <bool TAIL = false>
 __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__restrict__ out,
-                                                      const DevObs *__restrict__ og = nullptr,
+                                                      const DevObs *og = nullptr,
                                                       const DevHand *__restrict__ Hg = nullptr,
                                                       DevObs *__restrict__ obs_out = nullptr,
                                                       int same_eval = 0,
@@ -870,7 +870,7 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
                                                       double *__restrict__ hist = nullptr,
                                                       const int *__restrict__ fail = nullptr,
                                                       const DevObs *__restrict__ seq_table = nullptr,
-                                                      DevObs *__restrict__ seq_obs = nullptr,
+                                                      DevObs *seq_obs = nullptr,  // aliases og
                                                       int *__restrict__ seq_cur = nullptr) {
     constexpr int CH = 2048;  // generations staged per pass
     // offline sequences (hpe_track_sequence_dev): the frame's history row and slot come
@@ -1040,11 +1040,14 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
     for (int c = t; c < (G + 1) * GMIN_SHARDS; c += HPE_NT) sw.gmin[(size_t)c * GMIN_STRIDE] = ~0ull;
     if (TAIL) {
         if (obs_out && t < (int)(sizeof(DevObs) / 8)) ((unsigned long long *)obs_out)[t] = obs_word;
-        if (seq_cur) {
-            // the next frame's descriptor for the next frame's kernels (stream order: they
-            // start after this kernel); the slot after the last is never read.  No table
-            // (resident raw sequences): the row alone advances -- the next frame's refine
-            // launch prepares raw frame row + 1 by it
+        // Offline sequences: the next frame's descriptor for the next frame's kernels (stream
+        // order: they start after this kernel); the slot after the last is never read.  No
+        // table (resident raw sequences): the row alone advances -- the next frame's refine
+        // launch prepares raw frame row + 1 by it.  og IS seq_obs in sequence mode, so the
+        // descriptor is overwritten only after every read of this frame's: at the
+        // end of each path below, behind a barrier where this kernel evaluates cal_cost.
+        auto stage_next = [&]() {
+            if (!seq_cur) return;
             const int nx = seq_slot + 1 < HPE_MAX_SLOTS ? seq_slot + 1 : seq_slot;
             if (seq_table && t < (int)(sizeof(DevObs) / 8))
                 ((unsigned long long *)seq_obs)[t] = ((const unsigned long long *)(seq_table + nx))[t];
@@ -1052,15 +1055,19 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
                 seq_cur[0] = seq_slot + 1;
                 seq_cur[1] = seq_cur[1] + 1;
             }
-        }
+        };
         if (failed) {
             if (t <= HPE_DOF) {
                 out[t] = __builtin_nan("");
                 if (hist) hist[t] = __builtin_nan("");
             }
+            stage_next();
             return;
         }
-        if (same_eval && last >= 0) return;  // out[26] = gcost = cal_cost(bestp)
+        if (same_eval && last >= 0) {  // out[26] = gcost = cal_cost(bestp)
+            stage_next();
+            return;
+        }
         const DevObs o = *og;
         if (t < HPE_DOF) sm.fk.th[t] = bp;
         const CloudGlobal cv = obs_cloud(o);
@@ -1071,6 +1078,8 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
             out[HPE_DOF] = c;
             if (hist) hist[HPE_DOF] = c;
         }
+        __syncthreads();  // every thread has read this frame's descriptor
+        stage_next();
     }
 }
 
@@ -1112,11 +1121,6 @@ struct __align__(16) RefineSm {
     double x0[32];
     double f[RF_NW];
     double fg[RF_NW];  // the gradient points' costs (k_refine, single-workgroup form)
-    // the speculated Goldstein nodes' own decisions (gold_decide): byte w = node w's code
-    // (0 down, 1 up, 2 accept), gpost[w] = its bracket {a, b, alpha} after the decision
-    // and its own alpha
-    unsigned long long gcode;
-    double gpost[RF_NW][4];
     FkX X;  // rotation-only joint terms of x0 (refine block 2: translation steps)
     RigidSm rg;  // hand-frame centres, block 2's rotated centres, collision (rigid refine)
     unsigned ts_n;  // diagnostic build: refine timeline entries written
@@ -1133,56 +1137,11 @@ __device__ __forceinline__ void gold_down(double a, double &b, double &alpha) {
     alpha = 0.5 * (a + alpha);
 }
 
-// A speculated node's Goldstein test (PSO.cpp:459-474), taken by the node's own wave right
-// after its evaluation with the same operations the serial search applies at that node
-// (its bracket state replayed from the round's start): the walk then follows byte codes
-// and reads one post-state instead of redoing the fp64 tests level by level.
-// Two round-4 variants of the Goldstein round, both exact, both measured no faster (A/B on
-// one box, 3 x 40 frames: refine 145.5 us with neither, 148.4 with both, 145.2 / 148.3
-// with one each): the nodes taking their own tests so the walk follows byte
-// codes (HPE_GOLD_CODED=1), and the rigid node as one fused function placing its matched
-// centres in registers (HPE_RIGID_FUSED=1).  Off by default.
-#ifndef HPE_GOLD_CODED
-#define HPE_GOLD_CODED 0
-#endif
+// The hand-frame form's correspondence search takes one item on every wave (round 4: the
+// chain form's spread balanced the SIMDs against the gradient heads' DH chains).
 #ifndef HPE_RF_SPREAD
 #define HPE_RF_SPREAD 1
 #endif
-#ifndef HPE_RF_HEAD_FIRST
-#define HPE_RF_HEAD_FIRST 0
-#endif
-#ifndef HPE_RIGID_FUSED
-#define HPE_RIGID_FUSED 0
-#endif
-struct GoldIn {
-    double fk, gp;  // f_k and g'p of the search
-    double a, b, al;  // this node's bracket state before its test (al = its alpha)
-};
-__device__ __forceinline__ void gold_decide(unsigned long long *codes, double (*post)[4], int w,
-                                            double f1, const GoldIn &g) {
-    const double armijo = g.fk + 0.25 * g.al * g.gp;
-    const double gold = g.fk + (1 - 0.25) * g.al * g.gp;
-    double a = g.a, b = g.b, alpha = g.al;
-    unsigned code;
-    if (f1 <= armijo) {
-        if (f1 >= gold) {
-            code = 2;
-        } else {
-            code = 1;
-            gold_up(a, b, alpha);
-        }
-    } else {
-        code = 0;
-        gold_down(a, b, alpha);
-    }
-    if ((threadIdx.x & 63) == 0) {
-        ((unsigned char *)codes)[w] = (unsigned char)code;
-        post[w][0] = a;
-        post[w][1] = b;
-        post[w][2] = alpha;
-        post[w][3] = g.al;
-    }
-}
 
 // ---------------------------------------------------------------- multi-workgroup refine
 // For clouds larger than RF_STAGE_MAX one CU is throughput-bound (every Goldstein round is
@@ -1269,24 +1228,19 @@ __device__ __forceinline__ double mw_sum(const MwLeader &ml, int w) {
 // own rs.w[w].th.  Ends with a workgroup barrier.
 // RIGID: the nodes' spheres by rigid_wave (rblk 0: rotation block, 1: translation block),
 // the collision the constant rs.rg.C.
-// gin (Goldstein nodes): each node wave also takes its own test (gold_decide).
 template <bool MW, bool RIGID = false, class CV>
 __device__ __forceinline__ void eval_nodes(RefineSm &rs, int nn, const DevObs &o, const CV &cv,
                                            const DevHand *__restrict__ H,
                                            const int32_t *__restrict__ match, FkX *Xt,
                                            MwLeader *ml, int *flag, const double *thr = nullptr,
                                            const FrozenPts *fp = nullptr, int rblk = 0,
-                                           const GoldIn *gin = nullptr,
                                            const double *md2p = nullptr) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     if (!MW) {
         if (w < nn) {
             wave_sync();
             double f;
-            if (RIGID && fp && HPE_RIGID_FUSED) {  // small clouds: the fused node
-                f = rblk ? rigid_node<RG_TRANS>(rs.w[w], o, cv, H, rs.rg, *thr, *fp)
-                         : rigid_node<RG_ROT>(rs.w[w], o, cv, H, rs.rg, *thr, *fp);
-            } else if (RIGID) {
+            if (RIGID) {
                 const FrozenHead hd = rblk ? rigid_head<RG_TRANS>(rs.w[w], o, H, rs.rg, *thr)
                                            : rigid_head<RG_ROT>(rs.w[w], o, H, rs.rg, *thr);
                 f = frozen_tail<true>(rs.w[w], o, cv, H, match, hd, fp, md2p) + rs.rg.C;
@@ -1294,7 +1248,6 @@ __device__ __forceinline__ void eval_nodes(RefineSm &rs, int nn, const DevObs &o
                 f = eval_wave_frozen<true>(rs.w[w], o, cv, H, match, Xt, thr, fp);
             }
             if (l == 0) rs.f[w] = f;
-            if (gin) gold_decide(&rs.gcode, rs.gpost, w, f, *gin);
         }
         REF_TS(rs.ts_n, 9);  // wave 0's node done
         __syncthreads();
@@ -1325,7 +1278,6 @@ __device__ __forceinline__ void eval_nodes(RefineSm &rs, int nn, const DevObs &o
         const double f = RIGID ? (al * o.lambda + dep) + rs.rg.C : (al * o.lambda + dep) + co;
         const double fr = ml->failed ? __builtin_nan("") : f;
         if (l == 0) rs.f[w] = fr;
-        if (gin) gold_decide(&rs.gcode, rs.gpost, w, fr, *gin);
     }
     __syncthreads();
 }
@@ -1463,17 +1415,15 @@ struct GoldShape {
 };
 #define GOLD_BALANCED 0
 #define GOLD_8 1
-#define GOLD_7 2
-#define GOLD_4 3
-#define GOLD_OPT8 4  // pso_optimise's descent (tools/gold_shapes.py optimise)
-#define GOLD_MIX 5   // GOLD_8 after a search's start and a "down", GOLD_4 after an "up"
-#define GOLD_MIX2 6  // jointly fitted by round time: 8 nodes at a search's start, 4 after
+#define GOLD_4 2
+#define GOLD_OPT8 3  // pso_optimise's descent (tools/gold_shapes.py optimise)
+#define GOLD_MIX 4   // GOLD_8 after a search's start and a "down", GOLD_4 after an "up"
 #ifndef HPE_GOLD_POLICY
 #define HPE_GOLD_POLICY GOLD_MIX  // refine_init_pose
 #endif
 template <int POL>
 __device__ __forceinline__ GoldShape gold_shape(int ctx) {
-    constexpr GoldShape T[21] = {
+    constexpr GoldShape T[15] = {
     // GOLD_BALANCED
     {7, 0x0043414240212000ull, 0xfffff531u, 0xfffff642u},  // first: '' 'D' 'U' 'DD' 'DU' 'UD' 'UU'
     {7, 0x0043414240212000ull, 0xfffff531u, 0xfffff642u},  // D: '' 'D' 'U' 'DD' 'DU' 'UD' 'UU'
@@ -1482,10 +1432,6 @@ __device__ __forceinline__ GoldShape gold_shape(int ctx) {
     {8, 0xa080604340212000ull, 0xf76f5f31u, 0xfffff4f2u},  // first: '' 'D' 'U' 'DD' 'UU' 'DDD' 'DDDD' 'DDDDD'
     {8, 0x6043414240212000ull, 0xffff7531u, 0xfffff642u},  // D: '' 'D' 'U' 'DD' 'DU' 'UD' 'UU' 'DDD'
     {8, 0x6243414240212000ull, 0xfff7f531u, 0xfffff642u},  // U: '' 'D' 'U' 'DD' 'DU' 'UD' 'UU' 'DUD'
-    // GOLD_7
-    {7, 0x0080604340212000ull, 0xff6f5f31u, 0xfffff4f2u},  // first: '' 'D' 'U' 'DD' 'UU' 'DDD' 'DDDD'
-    {7, 0x0060414240212000ull, 0xffff6531u, 0xffffff42u},  // D: '' 'D' 'U' 'DD' 'DU' 'UD' 'DDD'
-    {7, 0x0043414240212000ull, 0xfffff531u, 0xfffff642u},  // U: '' 'D' 'U' 'DD' 'DU' 'UD' 'UU'
     // GOLD_4
     {4, 0x0000000043212000ull, 0xfffffff1u, 0xfffff3f2u},  // first: '' 'D' 'U' 'UU'
     {4, 0x0000000060402000ull, 0xfffff321u, 0xffffffffu},  // D: '' 'D' 'DD' 'DDD'
@@ -1497,10 +1443,6 @@ __device__ __forceinline__ GoldShape gold_shape(int ctx) {
     // GOLD_MIX (4 nodes, one wave per SIMD, run a round in ~0.71 of an 8-node one)
     {8, 0xa080604340212000ull, 0xf76f5f31u, 0xfffff4f2u},  // first: '' 'D' 'U' 'DD' 'UU' 'DDD' 'DDDD' 'DDDDD'
     {8, 0x6043414240212000ull, 0xffff7531u, 0xfffff642u},  // D: '' 'D' 'U' 'DD' 'DU' 'UD' 'UU' 'DDD'
-    {4, 0x0000000040212000ull, 0xffffff31u, 0xfffffff2u},  // U: '' 'D' 'U' 'DD'
-    // GOLD_MIX2 (tools/gold_shapes.py, joint fit by round time)
-    {8, 0xa080604340212000ull, 0xf76f5f31u, 0xfffff4f2u},  // first: '' 'D' 'U' 'DD' 'UU' 'DDD' 'DDDD' 'DDDDD'
-    {4, 0x0000000040212000ull, 0xffffff31u, 0xfffffff2u},  // D: '' 'D' 'U' 'DD'
     {4, 0x0000000040212000ull, 0xffffff31u, 0xfffffff2u},  // U: '' 'D' 'U' 'DD'
     };
     return ctx == 0 ? T[3 * POL] : ctx == 1 ? T[3 * POL + 1] : T[3 * POL + 2];
@@ -1533,20 +1475,18 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
         const GoldShape sh = gold_shape<POL>(ctx);
         const int nn = sh.n;
         double thl = 0.0;  // theta[l] of this wave's node (FK's trig reads it in a register)
-        GoldIn gin{fk, gp, A, B, alpha};
         if (w < nn) {
             const int nbw = (int)((sh.nb >> (8 * w)) & 0xff), len = nbw >> 5, bits = nbw & 31;
+            double ga = A, gb = B, gal = alpha;
             for (int k = 0; k < len; ++k) {
-                if ((bits >> k) & 1) gold_up(gin.a, gin.b, gin.al);
-                else gold_down(gin.a, gin.b, gin.al);
+                if ((bits >> k) & 1) gold_up(ga, gb, gal);
+                else gold_down(ga, gb, gal);
             }
-            thl = rs.x0[l < HPE_DOF ? l : 0] + gin.al * pl;
+            thl = rs.x0[l < HPE_DOF ? l : 0] + gal * pl;
             if (l < HPE_DOF) rs.w[w].th[l] = thl;
         }
-        eval_nodes<MW, RIGID>(rs, nn, o, cv, H, match, Xt, ml, flag, &thl, fp, rblk,
-                              HPE_GOLD_CODED ? &gin : nullptr, md2p);
+        eval_nodes<MW, RIGID>(rs, nn, o, cv, H, match, Xt, ml, flag, &thl, fp, rblk, md2p);
         if (MW && ml->failed) break;  // the launch is ending early (DevMw::err)
-#if !HPE_GOLD_CODED
         // the serial rules walked level by level on the nodes' costs
         int node = 0;
         accepted = -1;
@@ -1578,46 +1518,6 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
                 ctx = 1;
             }
         }
-#else
-        // the walk: every node took its own test (gold_decide), so the serial search's path
-        // through the shape is a chain of byte codes; the bracket state after the round is
-        // the post-state of the last node tested
-        const unsigned long long codes = rs.gcode;
-        int node = 0, lastn = -1;
-        accepted = -1;
-#pragma unroll
-        for (int lev = 0; lev < 6; ++lev) {  // the deepest shape path is 6 nodes
-            if (node >= 15 || done) break;
-            if (it >= 30) {
-                done = true;
-                tk = 0;
-                break;
-            }
-            ++it;
-            const unsigned code = (unsigned)(codes >> (8 * node)) & 0xffu;
-            lastn = node;
-            if (code == 2) {
-                done = true;
-                accepted = node;
-            } else if (code == 1) {
-                node = (int)((sh.up >> (4 * node)) & 15u);
-                ctx = 2;
-                if (HPE_STAMPS) path |= 1ull << (it - 1);
-                if (HPE_STAMPS && blockIdx.x == 0 && t == 0) hpe_stamps[8] += 1;
-            } else {
-                node = (int)((sh.dn >> (4 * node)) & 15u);
-                ctx = 1;
-                if (HPE_STAMPS && blockIdx.x == 0 && t == 0) hpe_stamps[7] += 1;
-            }
-        }
-        if (accepted >= 0) {
-            tk = rs.gpost[accepted][3];
-        } else if (lastn >= 0 && !done) {
-            A = rs.gpost[lastn][0];
-            B = rs.gpost[lastn][1];
-            alpha = rs.gpost[lastn][2];
-        }
-#endif
         if (!done && it >= 30) done = true;  // tk stays 0
         // x0 is read only before eval_nodes' barrier in a round
         if (UPD && done && t < HPE_DOF) rs.x0[t] = rs.x0[t] - tk * gl;
@@ -1815,10 +1715,6 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
                         else hd = frozen_head<true>(rs.w[w], o, H, Xt, &thl);
                     }
                 };
-                // HPE_RF_HEAD_FIRST (hand-frame form): the head before the search, so its
-                // depth gathers are in flight during the search
-                constexpr bool head_first = RIGID && HPE_RF_HEAD_FIRST;
-                if (head_first) head();
                 const DepthG dgc = depth_issue_w0(rs.base, o, H);
                 const bool young = w >= HPE_SETPRIO_FROM;  // as in eval_block
                 if (young) __builtin_amdgcn_s_setprio(1);
@@ -1842,7 +1738,7 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
                 const double dep = depth_finish(dgc, o, t < HPE_NS);
                 const double tot = wave_sum((al * o.lambda + dep) + co);  // as block_sum1
                 if (l == 0) rs.red[w][0] = tot;
-                if (!head_first) head();
+                head();
                 __syncthreads();  // matchId complete, the corr partial sums in red
                 if (small) load_frozen_pts(fpts, cv, match, l);
                 fk = 0;

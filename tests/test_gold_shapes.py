@@ -18,7 +18,7 @@ import pytest
 import hand_data
 
 SRC = hand_data.ROOT / "hand-pose-estimation_amd" / "csrc" / "hpe_kernels.hip"
-POLICIES = ("GOLD_BALANCED", "GOLD_8", "GOLD_7", "GOLD_4", "GOLD_OPT8", "GOLD_MIX", "GOLD_MIX2")
+POLICIES = ("GOLD_BALANCED", "GOLD_8", "GOLD_4", "GOLD_OPT8", "GOLD_MIX")
 
 
 def _tables():

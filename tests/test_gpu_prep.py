@@ -193,6 +193,61 @@ def test_sequence_tracking_like_oracle_and_per_frame(gh, oracle, ora_hand, np_ha
     assert bad(gh.ctx.h, P, 1, None, s0, n, 0, None) == hpe._lib.HPE_E_ARG
 
 
+def test_sequence_wave_form_tail_and_empty_frame(gh, np_hand):
+    """in a sequence chunk the final kernel stages the next frame's
+    descriptor into the one its own cal_cost(bestp) tail reads.  The tail runs when the
+    generations used the wave form (P >= 1024: no same-eval shortcut) or when no cost beat
+    1e100 (an empty frame: every cost NaN).  Every frame of the sequence must equal
+    hpe_track_frame_dev frame by frame, bit for bit, NaNs included."""
+    import ctypes as C
+    import hpe
+    import torch
+    n, P, maxiter, s0 = 5, 1024, 3, 600
+    poses = hand_data.trajectory(n, seed=29)
+    depth = [oracle_np.render_depth_mm(np_hand, th) for th in poses]
+    depth[2] = np.zeros_like(depth[2])  # empty frame: NaN scale, NaN costs, bestp = zeros
+    ub, lb, sd = oracle_np.reference_bounds()
+    pso = hpe.PSO()
+    pso.set_pso_params(ub, lb, sd, 0.7298, 1.49618, 1.49618, maxiter, 1e-8, 1e-8)
+    pso._push(gh.ctx)
+    for f in range(n):
+        gh.ctx.prepare_frame(s0 + f, depth[f])
+    rt = gh.ctx.lib
+    st = torch.zeros(27, dtype=torch.float64, device="cuda:0")
+    per_frame = []
+    for f in range(n):  # the frames tracked independently from X0 (refine off)
+        st[:26] = torch.from_numpy(oracle_np.X0)
+        gh.ctx.select_frame(s0 + f)
+        gh.ctx.check(rt.hpe_track_frame_dev(gh.ctx.h, P, 0, C.c_void_p(st.data_ptr())))
+        gh.ctx.check(rt.hpe_sync(gh.ctx.h))
+        per_frame.append(st.cpu().numpy().copy())
+    assert np.isnan(per_frame[2][26]) and not np.isnan(per_frame[1][26])
+    hist = torch.empty((1, 27), dtype=torch.float64, device="cuda:0")
+    for f in range(n):  # each frame as a one-frame sequence chunk that stages the next slot
+        st[:26] = torch.from_numpy(oracle_np.X0)
+        st[26] = 0.0
+        hist.fill_(-1.0)
+        torch.cuda.synchronize()
+        gh.ctx.track_sequence(P, 0, st.data_ptr(), s0 + f, 1, 1, hist.data_ptr())
+        gh.ctx.check(rt.hpe_sync(gh.ctx.h))
+        assert np.array_equal(hist.cpu().numpy()[0], per_frame[f], equal_nan=True), f
+    # and the whole sequence in one chunk (x0 chained): the same bits as the chained per-frame loop
+    st[:26] = torch.from_numpy(oracle_np.X0)
+    chained = []
+    for f in range(n):
+        gh.ctx.select_frame(s0 + f)
+        gh.ctx.check(rt.hpe_track_frame_dev(gh.ctx.h, P, 0, C.c_void_p(st.data_ptr())))
+        gh.ctx.check(rt.hpe_sync(gh.ctx.h))
+        chained.append(st.cpu().numpy().copy())
+    hist = torch.empty((n, 27), dtype=torch.float64, device="cuda:0")
+    st[:26] = torch.from_numpy(oracle_np.X0)
+    st[26] = 0.0
+    torch.cuda.synchronize()
+    gh.ctx.track_sequence(P, 0, st.data_ptr(), s0, n, 8, hist.data_ptr())
+    gh.ctx.check(rt.hpe_sync(gh.ctx.h))
+    assert np.array_equal(hist.cpu().numpy(), np.array(chained), equal_nan=True)
+
+
 @pytest.mark.parametrize("downsample", [True, False])
 def test_raw_sequence_like_pipelined_and_oracle(gh, oracle, ora_hand, np_hand, downsample):
     """hpe_track_raw_sequence_dev (raw frames resident in HBM, each next frame prepared inside
