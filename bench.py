@@ -132,6 +132,82 @@ def parse():
     return a
 
 
+# ------------------------------------------------------------------------- extra passes
+def extra_passes(args, ctx, lib, state, state0, raw, n_frames, P, refine, ds, world, rank, local):
+    """Diagnostic passes over the timed frames, after the timed region (never in `value`):
+      refine_exact_ms_per_step   the same loop with the reference-order refine (DH chain on
+                                 every evaluation, hpe_set_refine_exact(1))
+      per_frame_graph_ms_per_step (N = 1) the per-frame pipelined loop of the N > 1 lines (one
+                                 graph per frame, raw frames from host memory), so the driver's
+                                 1 -> N curve can be read in one loop form
+      scaling_baseline_ms_per_step (N > 1) every rank tracks the frames alone in that same
+                                 per-frame loop, no exchange; the max over ranks: the N = 1
+                                 figure of this loop form on these GPUs
+    Each pass runs the frames twice (graph captures in the first) and times the second."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    exact0 = int(lib.hpe_get_refine_exact(ctx.h))
+    team = os.environ.get("HPE_REFINE_TEAM", "0")
+    out = {"refine_form": ("chain: the reference's DH chain on every evaluation" if exact0 else
+                           "hand-frame: spheres Rg q + u from centres built once per call, FK "
+                           "within 1e-12 cm of the chain (DESIGN.md §2)"),
+           "refine_kernel": ("k_refine_team, leader + helper workgroups (hpe_team.hpp)" if team == "1"
+                             else "k_refine_team leader alone" if team == "solo" else
+                             "k_refine, one workgroup"),
+           "refine_exact_ms_per_step": None, "per_frame_graph_ms_per_step": None,
+           "scaling_baseline_ms_per_step": None,
+           "note": ("diagnostic passes after the timed region over the same frames (second of two "
+                    "runs each): refine_exact = reference-order refine; per_frame_graph = one "
+                    "graph per frame from host memory (the N > 1 loop form); scaling_baseline = "
+                    "that form on every rank alone, no exchange, max over ranks")}
+    if not refine:
+        return out
+    d_raw = None
+
+    def run(K2):
+        nonlocal d_raw
+        state.copy_(state0)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        if K2:
+            if d_raw is None:
+                d_raw = torch.from_numpy(np.ascontiguousarray(np.stack(raw), dtype=np.float32)).to(
+                    f"cuda:{local}")
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+            ctx.track_raw_sequence(P, refine, state.data_ptr(),
+                                   d_raw.data_ptr() + args.warmup * d_raw[0].numel() * 4, args.steps,
+                                   True, ds, frames_per_graph=K2)
+        else:
+            ctx.pipeline_begin(raw[args.warmup], True, ds)
+            for f in range(args.warmup, n_frames):
+                ctx.track_pipelined(P, refine, state.data_ptr(), raw[f + 1] if f + 1 < n_frames else None)
+        ctx.check(lib.hpe_sync(ctx.h))
+        return (time.perf_counter() - t0) / args.steps * 1e3
+
+    def twice(K2):
+        run(K2)
+        return run(K2)
+
+    K = args.frames_per_graph
+    ctx.check(lib.hpe_set_refine_exact(ctx.h, 1))
+    out["refine_exact_ms_per_step"] = twice(K) if world == 1 else None
+    ctx.check(lib.hpe_set_refine_exact(ctx.h, exact0))
+    if world == 1:
+        out["per_frame_graph_ms_per_step"] = twice(0)
+    else:
+        ms = torch.tensor([twice(0)], dtype=torch.float64)
+        if args.backend == "nccl":
+            ms = ms.to(f"cuda:{local}")
+        dist.all_reduce(ms, op=dist.ReduceOp.MAX)
+        out["scaling_baseline_ms_per_step"] = float(ms.cpu()[0])
+    state.copy_(state0)
+    torch.cuda.synchronize()
+    return out
+
+
 # ------------------------------------------------------------------------- launcher
 def _free_port():
     with socket.socket() as s:
@@ -613,6 +689,8 @@ def main():
                       "min_us": mn.value * 1e3, "max_us": mx.value * 1e3,
                       "total_ms": tot.value}
     ctx.check(lib.hpe_profile_enable(ctx.h, 0))
+    extra = extra_passes(args, ctx, lib, state, state0, raw, n_frames, P, refine, ds, world, rank,
+                         local)
     prof["frame_graph"] = {"launches": len(frame_us), "avg_us": sum(frame_us) / len(frame_us),
                            "min_us": min(frame_us), "max_us": max(frame_us),
                            "median_us": float(np.median(frame_us)),
@@ -684,6 +762,8 @@ def main():
                                       {"seed": args.seed, "revert": TRAJ_REVERT,
                                        "frames": n_frames}),
                        "cloud_points": n_pts, "refine": bool(refine),
+                       "refine_form": extra["refine_form"],
+                       "refine_kernel": extra["refine_kernel"],
                        "exchange": ("once per frame (best of N subswarms)" if not args.exchange_every
                                     else f"every {args.exchange_every} generations + per frame "
                                          "(ICP-PSO style, non-reference)"),
@@ -701,6 +781,10 @@ def main():
             "roofline": roof or None,
             "dominant_kernel": dominant,
             "roofline_kernels": kernels_rf,
+            "refine_exact_ms_per_step": extra["refine_exact_ms_per_step"],
+            "per_frame_graph_ms_per_step": extra["per_frame_graph_ms_per_step"],
+            "scaling_baseline_ms_per_step": extra["scaling_baseline_ms_per_step"],
+            "extra_passes_note": extra["note"],
             "refine_evals_per_frame": rev.value / max(ref_launches, 1),
             "kernels": prof,
             "host_us_per_step": host_s / args.steps * 1e6,

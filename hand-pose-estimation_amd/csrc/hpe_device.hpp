@@ -1002,7 +1002,7 @@ template <class CV>
 __device__ __forceinline__ void load_frozen_pts(FrozenPts &fp, const CV &cv,
                                                 const int32_t *__restrict__ match, int l) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) fp.id[k] = match[min(l + 64 * k, cv.n - 1)];
+    for (int k = 0; k < 4; ++k) fp.id[k] = cv.n > 0 ? match[min(l + 64 * k, cv.n - 1)] : 0;
 }
 // align_frozen over the lane's points (n <= FP_MAX): the same per-point operations
 template <class CV>
@@ -1012,7 +1012,7 @@ __device__ __forceinline__ double align_frozen_pts(const FkSm &f, const FrozenPt
     double px[4], py[4], pz[4], sx[4], sy[4], sz[4], sr[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const int q = min(l + 64 * k, cv.n - 1);
+        const int q = min(l + 64 * k, max(cv.n - 1, 0));  // (n = 0: every term masked below)
         px[k] = cv.cx[q];
         py[k] = cv.cy[q];
         pz[k] = cv.cz[q];

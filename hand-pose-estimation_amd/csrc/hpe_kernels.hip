@@ -884,7 +884,8 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
     }
     // a timed-out multi-workgroup refine (DevMw::err, set until the host has reported it):
     // this frame's result is undefined, so bestp and cost become NaN
-    const int failed = (TAIL && fail) ? __hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    const int failed = __builtin_amdgcn_readfirstlane(
+        (TAIL && fail) ? __hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0);
     __shared__ Smem sm;
     __shared__ double gm[CH];
     __shared__ int tp[CH];
@@ -901,6 +902,13 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
         __hip_atomic_store(done_host, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if (TAIL) stage_hand<HPE_NT>(sm.hand, Hg);
+    // this frame's descriptor, read before the tail stages the next frame's into it (og IS
+    // seq_obs in sequence mode).  (Staging the next descriptor after the tail's
+    // own evaluation instead, behind a barrier, miscompiled with ROCm 7.2: the early returns
+    // around that evaluation no longer skipped it, and the same-eval case's gcost was
+    // overwritten by a re-evaluated cost -- tools/ab_dump.py, round 5.)
+    DevObs o_early{};
+    if (TAIL) o_early = *og;
     // the frame descriptor handed back at the end, loaded now (off the final chain)
     const unsigned long long obs_word =
         (TAIL && obs_out && t < (int)(sizeof(DevObs) / 8)) ? ((const unsigned long long *)og)[t] : 0ull;
@@ -1040,14 +1048,7 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
     for (int c = t; c < (G + 1) * GMIN_SHARDS; c += HPE_NT) sw.gmin[(size_t)c * GMIN_STRIDE] = ~0ull;
     if (TAIL) {
         if (obs_out && t < (int)(sizeof(DevObs) / 8)) ((unsigned long long *)obs_out)[t] = obs_word;
-        // Offline sequences: the next frame's descriptor for the next frame's kernels (stream
-        // order: they start after this kernel); the slot after the last is never read.  No
-        // table (resident raw sequences): the row alone advances -- the next frame's refine
-        // launch prepares raw frame row + 1 by it.  og IS seq_obs in sequence mode, so the
-        // descriptor is overwritten only after every read of this frame's: at the
-        // end of each path below, behind a barrier where this kernel evaluates cal_cost.
-        auto stage_next = [&]() {
-            if (!seq_cur) return;
+        if (seq_cur) {
             const int nx = seq_slot + 1 < HPE_MAX_SLOTS ? seq_slot + 1 : seq_slot;
             if (seq_table && t < (int)(sizeof(DevObs) / 8))
                 ((unsigned long long *)seq_obs)[t] = ((const unsigned long long *)(seq_table + nx))[t];
@@ -1055,20 +1056,16 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
                 seq_cur[0] = seq_slot + 1;
                 seq_cur[1] = seq_cur[1] + 1;
             }
-        };
+        }
         if (failed) {
             if (t <= HPE_DOF) {
                 out[t] = __builtin_nan("");
                 if (hist) hist[t] = __builtin_nan("");
             }
-            stage_next();
             return;
         }
-        if (same_eval && last >= 0) {  // out[26] = gcost = cal_cost(bestp)
-            stage_next();
-            return;
-        }
-        const DevObs o = *og;
+        if (same_eval && last >= 0) return;  // out[26] = gcost = cal_cost(bestp)
+        const DevObs o = o_early;
         if (t < HPE_DOF) sm.fk.th[t] = bp;
         const CloudGlobal cv = obs_cloud(o);
         const Pt pre = load_pt(cv, t);
@@ -1078,8 +1075,6 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
             out[HPE_DOF] = c;
             if (hist) hist[HPE_DOF] = c;
         }
-        __syncthreads();  // every thread has read this frame's descriptor
-        stage_next();
     }
 }
 
@@ -1805,6 +1800,9 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
         atomicAdd((unsigned long long *)(evals_out + 2), (unsigned long long)evals);  // running total
     }
 }
+
+// ------------------------------------------------------------------ team refine
+#include "hpe_team.hpp"
 
 #include "hpe_optimise.hpp"
 

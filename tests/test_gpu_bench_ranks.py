@@ -47,6 +47,10 @@ def test_bench_two_ranks_same_device_gloo(tmp_path, oracle, ora_hand):
     assert rk["final_state_identical"]
     assert 0 < rk["ms_per_step_min"] <= rk["ms_per_step_max"]
     assert rk["exchange_us"]["frames"] == 3 and rk["exchange_us"]["mean"] > 0
+    # the N > 1 line carries the N = 1 figure of its own loop form and
+    # names the refine form it ran (item 5)
+    assert r["scaling_baseline_ms_per_step"] > 0 and r["per_frame_graph_ms_per_step"] is None
+    assert r["config"]["refine_form"] and r["config"]["refine_kernel"]
     st = [np.load(dump / f"states_rank{k}.npy") for k in range(2)]
     assert st[0].shape == (4, 27)
     np.testing.assert_array_equal(st[0], st[1])  # every rank adopts the same winner

@@ -35,12 +35,33 @@ SEQ_POSE_TOL, SEQ_COST_RTOL = 2e-6, 1e-7  # long sequences (test_config3)
 TIE_MARGIN = 1e-13
 
 
-def _tie_replay(oracle, ora_hand, obs, x0, gpu_evals):
+def _gpu_refine(gh, raw, x0, downsample=True):
+    """The GPU's refine_init_pose of one raw frame from x0 (the same kernel and operations as
+    inside the tracking loop): (refined pose, evaluation count)."""
+    import hpe
+    om = hpe.observedmodel()
+    om.downsample = downsample
+    om.set_depth_mm(raw)
+    cf = hpe.costfunc(gh, om)
+    x = np.array(x0, dtype=np.float64)
+    pso = hpe.PSO()
+    pso.refine_init_pose(x, cf)
+    return x, pso.last_refine_evals
+
+
+def _tie_replay(oracle, ora_hand, obs, x0, gpu_evals, gh=None, raw=None, rigid=REFINE_RIGID,
+                downsample=True):
     """A refine whose evaluation count differs from the oracle's must be the oracle's own
     run with near-tie decisions (margin < TIE_MARGIN) inverted: hand_data.tie_replay
     replays one, then two, flipped ties and returns the flips whose replay takes exactly
-    the GPU's evaluation count (None: no near-tie explains it)."""
-    return hand_data.tie_replay(oracle, ora_hand, obs, x0, gpu_evals, REFINE_RIGID, TIE_MARGIN)
+    the GPU's evaluation count AND reaches the GPU's refined pose within 1e-6 (the GPU's
+    refine of the same frame from the same x0, when gh / raw are given); None: no near-tie
+    explains it.  rigid=False replays the reference's operation order (the chain)."""
+    pose = None
+    if gh is not None:
+        pose, ev = _gpu_refine(gh, raw, x0, downsample)
+        assert ev == gpu_evals, (ev, gpu_evals)  # the loop's refine, reproduced
+    return hand_data.tie_replay(oracle, ora_hand, obs, x0, gpu_evals, rigid, TIE_MARGIN, pose=pose)
 
 
 @pytest.fixture(scope="module")
@@ -252,7 +273,8 @@ def test_config3_full_cloud_20_frames_pipelined(oracle, ora_hand, gh):
         dpose.append(np.abs(gx[f] - xr).max())
         assert _cost_eq(gc[f], cr, SEQ_COST_RTOL), (f, gc[f], cr)
         if gev[f] != er:
-            ev_mismatch.append((f, _tie_replay(oracle, ora_hand, obs, x0, gev[f])))
+            ev_mismatch.append((f, _tie_replay(oracle, ora_hand, obs, x0, gev[f], gh, raw[f],
+                                               downsample=False)))
     dpose, margin = np.array(dpose), np.array(margin)
     print(f"{n} full-cloud frames: max |dpose| {dpose.max():.3g} (frame {int(dpose.argmax())}), "
           f"refine eval-count mismatches (frame, flipped tie's margin) {ev_mismatch}; frames "
@@ -262,10 +284,61 @@ def test_config3_full_cloud_20_frames_pipelined(oracle, ora_hand, gh):
     assert all(m is not None for _, m in ev_mismatch), "an eval-count mismatch no near-tie explains"
 
 
-def test_config3_sequence_400_frames_pipelined(oracle, ora_hand, gh):
-    """BASELINE config 3: 400 tracked frames, 256 x 30, refine on, x0 <- previous bestp
-    (testmodel.cpp:117-139), through the pipelined loop of bench.py (raw float32 mm depth
-    in, preprocessing on the GPU inside the previous frame's refine launch).
+@pytest.fixture(scope="module")
+def seq400(gh):
+    """BASELINE config 3 on the GPU: 400 tracked frames, 256 x 30, refine on, x0 <- previous
+    bestp (testmodel.cpp:117-139), through the pipelined loop of bench.py (raw float32 mm
+    depth in, preprocessing on the GPU inside the previous frame's refine launch)."""
+    n, P, maxiter = 400, 256, 31
+    poses = hand_data.trajectory(n, seed=7, revert=0.02)  # stays in view
+    raw = [np.ascontiguousarray(gh.ctx.render_depth(th)) for th in poses]
+    gx, gc, gev = _track_pipelined(gh, raw, P, maxiter, poses[0], True)
+    return dict(n=n, P=P, maxiter=maxiter, poses=poses, raw=raw, gx=gx, gc=gc, gev=gev)
+
+
+def _seq400_check(oracle, ora_hand, gh, s, rigid):
+    """Every frame against the oracle (rigid: the mirror of the GPU's hand-frame refine;
+    not rigid: the reference's own operation order, the DH chain on every evaluation)
+    started from the GPU's previous pose, and the oracle running free over the sequence."""
+    n, P, maxiter, poses, raw, gx, gc, gev = (s[k] for k in ("n", "P", "maxiter", "poses", "raw",
+                                                            "gx", "gc", "gev"))
+    ub, lb, sd = oracle_np.reference_bounds()
+    free = poses[0].copy()
+    dpose, dcost, drift, ev_mismatch, margin = [], [], [], [], []
+    for f in range(n):
+        obs = oracle.preprocess(raw[f])
+        x0 = poses[0] if f == 0 else gx[f - 1]
+        xr, er = oracle.refine(ora_hand, obs, x0, rigid=rigid)
+        margin.append(oracle.refine_last_margin())
+        xr, _, _ = oracle.pso_evolve(ora_hand, obs, xr, P, maxiter, lb, ub, sd, seed=1000)
+        cr = oracle.cal_cost(ora_hand, obs, xr)
+        dpose.append(np.abs(gx[f] - xr).max())
+        dcost.append(0.0 if _cost_eq(gc[f], cr, SEQ_COST_RTOL) and np.isnan(cr)
+                     else abs(gc[f] - cr) / abs(cr))
+        if gev[f] != er:
+            ev_mismatch.append((f, _tie_replay(oracle, ora_hand, obs, x0, gev[f], gh, raw[f], rigid)))
+        free, _ = oracle.refine(ora_hand, obs, free, rigid=rigid)
+        free, _, _ = oracle.pso_evolve(ora_hand, obs, free, P, maxiter, lb, ub, sd, seed=1000)
+        drift.append(np.abs(free - gx[f]).max())
+    dpose, dcost, drift, margin = np.array(dpose), np.array(dcost), np.array(drift), np.array(margin)
+    first = lambda a, t: (int(np.nonzero(a > t)[0][0]) if (a > t).any() else None)  # noqa: E731
+    flips = max((len(m) for _, m in ev_mismatch if m is not None), default=0)
+    print(f"400 frames vs the oracle's {'hand-frame mirror' if rigid else 'reference order (chain)'}: "
+          f"per-frame max |dpose| {dpose.max():.3g} (frame {int(dpose.argmax())}), max dcost "
+          f"{np.nanmax(dcost):.3g}, refine eval-count mismatches {len(ev_mismatch)}, most flips a "
+          f"frame needed {flips}; free-running oracle: max drift {drift.max():.3g}, first frame "
+          f"beyond {POSE_TOL:g}: {first(drift, POSE_TOL)}; mismatched frames (frame, flipped "
+          f"ties (decision, margin)) {ev_mismatch}; frames with a margin < {TIE_MARGIN:g}: "
+          f"{int((margin < TIE_MARGIN).sum())}, median margin {np.median(margin):.3g}")
+    assert dpose.max() <= SEQ_POSE_TOL, f"frame {int(dpose.argmax())}: pose {dpose.max()}"
+    assert np.all(dcost <= SEQ_COST_RTOL), f"frame {int(np.nanargmax(dcost))}: cost {dcost.max()}"
+    assert len(ev_mismatch) <= n // 20
+    assert all(m is not None for _, m in ev_mismatch), "an eval-count mismatch no near-tie explains"
+    assert drift.max() <= 10 * SEQ_POSE_TOL, f"free-running divergence from frame {first(drift, 10 * SEQ_POSE_TOL)}"
+
+
+def test_config3_sequence_400_frames_pipelined(oracle, ora_hand, gh, seq400):
+    """BASELINE config 3 (seq400) against the oracle's mirror of the GPU's refine form.
 
     Checked two ways: (1) every frame against the oracle started from the GPU's previous
     pose (per-frame parity, no accumulated history); (2) the oracle running free over the
@@ -277,45 +350,20 @@ def test_config3_sequence_400_frames_pipelined(oracle, ora_hand, gh):
     ~1e-13: on ~2 % of frames a decision flips, the refine takes a few evaluations more or
     fewer and the pose moves by up to ~1e-6 (measured on this sequence: 9 of 400 frames,
     max 9.6e-7; free-running drift max 3.5e-7).  Each such frame must
-    be the oracle's refine from the same x0 with one near-tie decision (relative margin
-    below TIE_MARGIN) inverted: replaying the oracle with that decision flipped takes
-    exactly the GPU's evaluation count (_tie_replay).  Single calls keep the exact eval count
-    (test_gpu_parity.py)."""
-    n, P, maxiter = 400, 256, 31
-    poses = hand_data.trajectory(n, seed=7, revert=0.02)  # stays in view
-    raw = [np.ascontiguousarray(gh.ctx.render_depth(th)) for th in poses]
-    gx, gc, gev = _track_pipelined(gh, raw, P, maxiter, poses[0], True)
-    ub, lb, sd = oracle_np.reference_bounds()
-    free = poses[0].copy()
-    dpose, dcost, drift, ev_mismatch, margin = [], [], [], [], []
-    for f in range(n):
-        obs = oracle.preprocess(raw[f])
-        x0 = poses[0] if f == 0 else gx[f - 1]
-        xr, er = oracle.refine(ora_hand, obs, x0, rigid=REFINE_RIGID)
-        margin.append(oracle.refine_last_margin())
-        xr, _, _ = oracle.pso_evolve(ora_hand, obs, xr, P, maxiter, lb, ub, sd, seed=1000)
-        cr = oracle.cal_cost(ora_hand, obs, xr)
-        dpose.append(np.abs(gx[f] - xr).max())
-        dcost.append(0.0 if _cost_eq(gc[f], cr, SEQ_COST_RTOL) and np.isnan(cr)
-                     else abs(gc[f] - cr) / abs(cr))
-        if gev[f] != er:
-            ev_mismatch.append((f, _tie_replay(oracle, ora_hand, obs, x0, gev[f])))
-        free, _ = oracle.refine(ora_hand, obs, free, rigid=REFINE_RIGID)
-        free, _, _ = oracle.pso_evolve(ora_hand, obs, free, P, maxiter, lb, ub, sd, seed=1000)
-        drift.append(np.abs(free - gx[f]).max())
-    dpose, dcost, drift, margin = np.array(dpose), np.array(dcost), np.array(drift), np.array(margin)
-    first = lambda a, t: (int(np.nonzero(a > t)[0][0]) if (a > t).any() else None)  # noqa: E731
-    print(f"400 frames: per-frame max |dpose| {dpose.max():.3g} (frame {int(dpose.argmax())}), "
-          f"max dcost {np.nanmax(dcost):.3g}, refine eval-count mismatches {len(ev_mismatch)} "
-          f"{ev_mismatch[:10]}; free-running oracle: max drift {drift.max():.3g}, first frame "
-          f"beyond {POSE_TOL:g}: {first(drift, POSE_TOL)}; mismatched frames (frame, flipped "
-          f"tie's margin) {ev_mismatch}; frames with a margin < {TIE_MARGIN:g}: "
-          f"{int((margin < TIE_MARGIN).sum())}, median margin {np.median(margin):.3g}")
-    assert dpose.max() <= SEQ_POSE_TOL, f"frame {int(dpose.argmax())}: pose {dpose.max()}"
-    assert np.all(dcost <= SEQ_COST_RTOL), f"frame {int(np.nanargmax(dcost))}: cost {dcost.max()}"
-    assert len(ev_mismatch) <= n // 20
-    assert all(m is not None for _, m in ev_mismatch), "an eval-count mismatch no near-tie explains"
-    assert drift.max() <= 10 * SEQ_POSE_TOL, f"free-running divergence from frame {first(drift, 10 * SEQ_POSE_TOL)}"
+    be the oracle's refine from the same x0 with one or two near-tie decisions (relative
+    margin below TIE_MARGIN) inverted: replaying the oracle with them flipped takes exactly
+    the GPU's evaluation count and reaches the GPU's refined pose (_tie_replay).  Single
+    calls keep the exact eval count (test_gpu_parity.py)."""
+    _seq400_check(oracle, ora_hand, gh, seq400, REFINE_RIGID)
+
+
+def test_config3_sequence_400_frames_vs_reference_order(oracle, ora_hand, gh, seq400):
+    """the same 400 GPU frames against the reference's own operation
+    order -- the oracle's restatement of refine_init_pose with the DH chain on every
+    evaluation (fingermodel.cpp:287-311 via handmodel.cpp:259-298, PSO.cpp:216-266) -- per
+    frame and free-running, with the same tolerances.  An eval-count mismatch must be a
+    replay of the chain refine with near-ties flipped that reaches the GPU's refined pose."""
+    _seq400_check(oracle, ora_hand, gh, seq400, False)
 
 
 def test_config1_hpe_track_32x10(tmp_path, oracle, ora_hand, np_hand):
