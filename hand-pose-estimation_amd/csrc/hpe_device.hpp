@@ -778,16 +778,14 @@ struct BfOut {
     int idx, ic;
     double cx, cy, cz, cr;
 };
-__device__ __forceinline__ BfOut bf_search(const FkSm &f, const DevHand *__restrict__ H,
-                                           const float *SX, const float *SY, const float *SZ,
-                                           float qx, float qy, float qz, int h,
-                                           int g_ts = BT_GENS) {
+// fp32 squared distances of the query (qx, qy, qz) to the 24 centres SX/SY/SZ[0..23] (two
+// per packed op: the same IEEE results as the scalar form), and their minimum.
+__device__ __forceinline__ float bf_d2_24(const float *SX, const float *SY, const float *SZ,
+                                          float qx, float qy, float qz, float (&d2)[24]) {
     typedef float f2 __attribute__((ext_vector_type(2)));  // packed fp32 (v_pk_*_f32)
-    float d2[24];
-    float m = __builtin_inff();
     const f2 q2x = {qx, qx}, q2y = {qy, qy}, q2z = {qz, qz};
 #pragma unroll
-    for (int j = 0; j < 24; j += 2) {  // two spheres per packed op, same IEEE results
+    for (int j = 0; j < 24; j += 2) {
         const f2 sx = *(const f2 *)(SX + j), sy = *(const f2 *)(SY + j),
                  sz = *(const f2 *)(SZ + j);
         const f2 t0 = q2x - sx, t1 = q2y - sy, t2 = q2z - sz;
@@ -795,31 +793,41 @@ __device__ __forceinline__ BfOut bf_search(const FkSm &f, const DevHand *__restr
         d2[j] = d.x;
         d2[j + 1] = d.y;
     }
-    {  // minimum as a three-level tree of 3-way mins (v_min3_f32), not a 12-deep chain
-        float m3[8];
+    // minimum as a three-level tree of 3-way mins (v_min3_f32), not a 12-deep chain
+    float m3[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) m3[k] = fminf(fminf(d2[3 * k], d2[3 * k + 1]), d2[3 * k + 2]);
-        m = fminf(fminf(fminf(m3[0], m3[1]), m3[2]), fminf(fminf(m3[3], m3[4]), m3[5]));
-        m = fminf(m, fminf(m3[6], m3[7]));
-    }
+    for (int k = 0; k < 8; ++k) m3[k] = fminf(fminf(d2[3 * k], d2[3 * k + 1]), d2[3 * k + 2]);
+    float m = fminf(fminf(fminf(m3[0], m3[1]), m3[2]), fminf(fminf(m3[3], m3[4]), m3[5]));
+    return fminf(m, fminf(m3[6], m3[7]));
+}
+// first j in 0..23 with bits(d2[j]) <= hb, branch-free: key_j = j, or j | 2^31 when
+// d2[j] > hb (non-negative floats order like their bit patterns), then an unsigned min
+// tree.  Returns the smallest key (>= 64: no such j).
+__device__ __forceinline__ unsigned bf_first_le_24(const float (&d2)[24], int hb) {
+    unsigned key[24];
+#define HPE_KEY(J) key[J] = sqrt_class_key<J>(hb, d2[J]);
+    HPE_KEY(0) HPE_KEY(1) HPE_KEY(2) HPE_KEY(3) HPE_KEY(4) HPE_KEY(5) HPE_KEY(6) HPE_KEY(7)
+    HPE_KEY(8) HPE_KEY(9) HPE_KEY(10) HPE_KEY(11) HPE_KEY(12) HPE_KEY(13) HPE_KEY(14)
+    HPE_KEY(15) HPE_KEY(16) HPE_KEY(17) HPE_KEY(18) HPE_KEY(19) HPE_KEY(20) HPE_KEY(21)
+    HPE_KEY(22) HPE_KEY(23)
+#undef HPE_KEY
+#pragma unroll
+    for (int j = 0; j < 24; j += 3) key[j] = min(min(key[j], key[j + 1]), key[j + 2]);
+    return min(min(min(key[0], key[3]), min(key[6], key[9])),
+               min(min(key[12], key[15]), min(key[18], key[21])));
+}
+__device__ __forceinline__ BfOut bf_search(const FkSm &f, const DevHand *__restrict__ H,
+                                           const float *SX, const float *SY, const float *SZ,
+                                           float qx, float qy, float qz, int h,
+                                           int g_ts = BT_GENS) {
+    float d2[24];
+    float m = bf_d2_24(SX, SY, SZ, qx, qy, qz, d2);
     BLK_TS(g_ts, 11);
     m = fminf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0xB1, 0xf, 0xf,
                                                            false)));  // partner lane t^1
-    // first j with bits(d2[j]) <= hb, branch-free: key_j = j, or j | 2^31 when
-    // d2[j] > hb (non-negative floats order like their bit patterns), then an
-    // unsigned min tree and the partner lane's half
+    // the first j of this half at or below hb, then the partner lane's half
     auto first_le = [&](int hb) {
-        unsigned key[24];
-#define HPE_KEY(J) key[J] = sqrt_class_key<J>(hb, d2[J]);
-        HPE_KEY(0) HPE_KEY(1) HPE_KEY(2) HPE_KEY(3) HPE_KEY(4) HPE_KEY(5) HPE_KEY(6) HPE_KEY(7)
-        HPE_KEY(8) HPE_KEY(9) HPE_KEY(10) HPE_KEY(11) HPE_KEY(12) HPE_KEY(13) HPE_KEY(14)
-        HPE_KEY(15) HPE_KEY(16) HPE_KEY(17) HPE_KEY(18) HPE_KEY(19) HPE_KEY(20) HPE_KEY(21)
-        HPE_KEY(22) HPE_KEY(23)
-#undef HPE_KEY
-#pragma unroll
-        for (int j = 0; j < 24; j += 3) key[j] = min(min(key[j], key[j + 1]), key[j + 2]);
-        const unsigned kx = min(min(min(key[0], key[3]), min(key[6], key[9])),
-                                min(min(key[12], key[15]), min(key[18], key[21])));
+        const unsigned kx = bf_first_le_24(d2, hb);
         const int ix = (kx >= 64u) ? (1 << 20) : (int)kx + 24 * h;
         return min(ix, __builtin_amdgcn_mov_dpp(ix, 0xB1, 0xf, 0xf, false));
     };
@@ -921,6 +929,72 @@ __device__ __forceinline__ double search_align(const FkSm &f, const CV &cv,
         int k = 0;
         for (int it = gt; it < 2 * cv.n && k < max_items; it += stride, ++k)
             item(it, it == gt ? pre : load_pt(cv, it));
+    }
+    return acc;
+}
+
+// BFMatcher's match for one point by ONE lane over all 48 centres (the wave form's search:
+// no partner lane, so nothing a lane does per point is repeated by a second lane), as two
+// halves of 24 with d2 in registers one half at a time.  Half X's candidate cX is its first
+// j within 5 ulps of its own minimum mX.  If mA <= mB, m = mA and the whole search's first
+// j within 5 ulps of m lies in A (A's minimum qualifies): cA.  If mA > mB + 5 ulps, no
+// centre of A is within 5 ulps of m = mB: cB.  Either way the candidate equals bf_search's
+// first pass and is the match when its d2 IS m (the same check); otherwise, or when the
+// two minima are within 5 ulps of each other, the exact class is taken over both halves
+// again (rare).
+__device__ __forceinline__ BfOut bf_search_lane(const FkSm &f, const DevHand *__restrict__ H,
+                                                float qx, float qy, float qz) {
+    float d2[24];
+    const float mA = bf_d2_24(f.Sp[0], f.Sp[1], f.Sp[2], qx, qy, qz, d2);
+    const unsigned kA = bf_first_le_24(d2, __float_as_int(mA) + 5);
+    const float mB = bf_d2_24(f.Sp[0] + 24, f.Sp[1] + 24, f.Sp[2] + 24, qx, qy, qz, d2);
+    const unsigned kB = bf_first_le_24(d2, __float_as_int(mB) + 5);
+    const float m = fminf(mA, mB);
+    int idx = (mA <= mB) ? (int)kA : (__float_as_int(mA) > __float_as_int(mB) + 5) ? (int)kB + 24 : 64;
+    int ic = idx < HPE_NS ? idx : 0;
+    double cx = f.S[ic][0], cy = f.S[ic][1], cz = f.S[ic][2], cr = H->radii[ic];
+    const float tx = qx - (float)cx, ty = qy - (float)cy, tz = qz - (float)cz;
+    const float dc = (tx * tx + ty * ty) + tz * tz;
+    if (!(idx < HPE_NS && dc == m)) {  // (false for NaN)
+        const int hb = __float_as_int(hi_sqrt_class(m));
+        bf_d2_24(f.Sp[0], f.Sp[1], f.Sp[2], qx, qy, qz, d2);
+        const unsigned xa = bf_first_le_24(d2, hb);
+        bf_d2_24(f.Sp[0] + 24, f.Sp[1] + 24, f.Sp[2] + 24, qx, qy, qz, d2);
+        const unsigned xb = bf_first_le_24(d2, hb);
+        idx = (xa < 64u) ? (int)xa : (xb < 64u) ? (int)xb + 24 : (1 << 20);
+        ic = idx < HPE_NS ? idx : 0;  // >= 48: all-NaN point (reference undefined)
+        cx = f.S[ic][0];
+        cy = f.S[ic][1];
+        cz = f.S[ic][2];
+        cr = H->radii[ic];
+    }
+    return BfOut{idx, ic, cx, cy, cz, cr};
+}
+
+// The wave form's fused search + alignment (costfunc.cpp:306-377): lane l takes points
+// l, l + 64, ... of an HBM cloud, the next point loaded one ahead; returns the lane's
+// partial sum of (|p - S[m]| - r[m])^2.  pre = load_pt1(cv, lane).
+template <class CV>
+__device__ __forceinline__ Pt load_pt1(const CV &cv, int p) {
+    if (p < cv.n) return Pt{cv.cx[p], cv.cy[p], cv.cz[p]};
+    return Pt{0, 0, 0};
+}
+template <class CV>
+__device__ __forceinline__ double search_align_lane(const FkSm &f, const CV &cv,
+                                                    const DevHand *__restrict__ H, Pt pre) {
+    double acc = 0.0;
+    Pt q = pre;
+    for (int p = threadIdx.x & 63; p < cv.n; p += 64) {
+        // the centres are re-read from LDS per point (broadcast reads): hoisted out of the
+        // loop, the 144 floats would take the registers of every other wave on the SIMD
+        asm volatile("" ::: "memory");
+        const int pn = min(p + 64, cv.n - 1);
+        const Pt qn = Pt{cv.cx[pn], cv.cy[pn], cv.cz[pn]};
+        const BfOut r = bf_search_lane(f, H, (float)q.x, (float)q.y, (float)q.z);
+        const double dx = q.x - r.cx, dy = q.y - r.cy, dz = q.z - r.cz;
+        const double e = sqrt((dx * dx + dy * dy) + dz * dz) - r.cr;
+        acc += e * e;
+        q = qn;
     }
     return acc;
 }
@@ -1054,7 +1128,7 @@ enum EvalMode { EV_COST = 0, EV_COST2_CORR = 1, EV_COST2_FROZEN = 2, EV_COST_STO
 
 // cal_cost of the particle in f.th by ONE wave (FK + search over 64 lanes): the
 // throughput form used when there are many more particles than CUs.  All lanes return
-// the total; pre = load_pt(cv, lane).
+// the total; pre = load_pt1(cv, lane).
 template <class CV>
 __device__ __forceinline__ double eval_wave_cost(FkSm &f, const DevObs &o, const CV &cv,
                                                  const DevHand *__restrict__ H, Pt pre) {
@@ -1062,7 +1136,7 @@ __device__ __forceinline__ double eval_wave_cost(FkSm &f, const DevObs &o, const
     SphXYZ own;
     fk_wave(f, H, &own);
     const DepthG dg = depth_issue_at(own, l, o, H);
-    double al = search_align<64, false>(f, cv, H, nullptr, pre, l);
+    double al = search_align_lane(f, cv, H, pre);
     double dep = depth_finish(dg, o, l < HPE_NS);
     return wave_sum(al * o.lambda + dep);
 }

@@ -618,7 +618,7 @@ __global__ __launch_bounds__(PW_NT) void k_pso_init_w(DevSwarm sw, const double 
     Link lk[3];
     push_lane_links(sw, 0, ic, l, 1, -1, lk);
     const CloudGlobal cv = obs_cloud(o);
-    const Pt pre = load_pt(cv, l);
+    const Pt pre = load_pt1(cv, l);
     const double *sd = sw.bounds + 2 * HPE_DOF;
     if (sw.ext && blockIdx.x == 0 && t == 0) sw.ext[HPE_DOF] = __builtin_inf();  // no candidate yet
     if (l < HPE_DOF) {  // particles = x0 + randn % std (PSO.cpp:67-72)
@@ -666,7 +666,7 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
     // (the push links are loaded after the evaluation: held across it they would take the
     // registers of a third wave per SIMD; the other waves hide that load)
     const CloudGlobal cv = obs_cloud(o);
-    const Pt pre = load_pt(cv, l);
+    const Pt pre = load_pt1(cv, l);
     const size_t e = (size_t)ic * HPE_DOF + l;
     const size_t ec = (size_t)ic * HPE_DOF + (l < HPE_DOF ? l : HPE_DOF - 1);
     const double xo = sw.xh[(size_t)(g - 1) * P * HPE_DOF + ec];

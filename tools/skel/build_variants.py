@@ -1,0 +1,53 @@
+"""Diagnostic: phase-skeleton builds of the wave-form generation (k_pso_gen_w) for SQ
+instruction attribution.  Each variant is the product source with ONE
+phase compiled out (results invalid), built into hand-pose-estimation_amd/libhpe_skel_<v>.so
+for tools/skel/run_sq.sh (HPE_LIB_VARIANT).  The product source is not modified.
+Usage: python tools/skel/build_variants.py [variant ...]"""
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[2]
+PKG = ROOT / "hand-pose-estimation_amd"
+EDITS = {
+    "base": [],
+    # FK: the spheres stay whatever the workspace held (no sincos, no chain)
+    "nofk": [("hpe_device.hpp", "    SphXYZ own;\n    fk_wave(f, H, &own);\n    const DepthG dg = depth_issue_at(own, l, o, H);",
+              "    SphXYZ own{0.0, 0.0, 0.0};\n    const DepthG dg = depth_issue_at(own, l, o, H);")],
+    # the correspondence search + alignment
+    "nosearch": [("hpe_device.hpp", "    double al = search_align_lane(f, cv, H, pre);",
+                  "    double al = 0.0;")],
+    # the fp64 alignment residual inside the search (the match is still found)
+    "noalign": [("hpe_device.hpp", "        const double e = sqrt((dx * dx + dy * dy) + dz * dz) - r.cr;\n        acc += e * e;\n        q = qn;",
+                 "        acc += dx + (dy + dz);\n        q = qn;")],
+    # the rp / rg draws of the wave form
+    "nophilox": [("hpe_kernels.hip", "    const double rp = philox_u01(sw.seed, ST_RP, g, ic, dl);\n    const double rg = philox_u01(sw.seed, ST_RG, g, ic, dl);",
+                  "    const double rp = 0.25 + dl * 1e-3, rg = 0.75 - dl * 1e-3;")],
+}
+
+
+def build(v):
+    d = Path(f"/tmp/skel_{v}")
+    if d.exists():
+        shutil.rmtree(d)
+    (d / "hand-pose-estimation_amd").mkdir(parents=True)
+    shutil.copytree(PKG / "csrc", d / "hand-pose-estimation_amd" / "csrc")
+    shutil.copytree(ROOT / "include", d / "include")
+    for f, old, new in EDITS[v]:
+        p = d / "hand-pose-estimation_amd" / "csrc" / f
+        s = p.read_text()
+        assert s.count(old) == 1, (v, f, old[:60])
+        p.write_text(s.replace(old, new))
+    out = PKG / f"libhpe_skel_{v}.so"
+    cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-slp-vectorize",
+           "--offload-arch=gfx950", "-shared", "-o", str(out), "csrc/hpe_kernels.hip", "csrc/hpe_host.cpp"]
+    subprocess.run(cmd, cwd=d / "hand-pose-estimation_amd", check=True)
+    print(v, out)
+
+
+if __name__ == "__main__":
+    vs = sys.argv[1:] or list(EDITS)
+    procs = []
+    for v in vs:
+        build(v)
