@@ -45,14 +45,32 @@ __device__ unsigned long long hpe_blk_ts[BT_GENS * BT_BLK * BT_PTS];
         if (threadIdx.x == 0 && (g) < BT_GENS && blockIdx.x < BT_BLK)                      \
             hpe_blk_ts[((g) * BT_BLK + blockIdx.x) * BT_PTS + (k)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
-// the same from lane 0 of every wave (point k + wave)
+// the same from lane 0 of every wave (point k + wave) of every (gridDim.x / BT_BLK)-th
+// workgroup (a sample spread over the grid)
 #define WAVE_TS(g, k)                                                                      \
     do {                                                                                   \
-        if ((threadIdx.x & 63) == 0 && (g) < BT_GENS && blockIdx.x < BT_BLK)               \
-            hpe_blk_ts[((g) * BT_BLK + blockIdx.x) * BT_PTS + (k) + (threadIdx.x >> 6)] =  \
+        const unsigned st_ = (gridDim.x + BT_BLK - 1) / BT_BLK;                            \
+        if ((threadIdx.x & 63) == 0 && (g) < BT_GENS && blockIdx.x % st_ == 0)             \
+            hpe_blk_ts[((g) * BT_BLK + blockIdx.x / st_) * BT_PTS + (k) + (threadIdx.x >> 6)] = \
                 __builtin_amdgcn_s_memrealtime();                                          \
     } while (0)
+// the entry stamp with the wave's placement: low 40 bits of the 100 MHz clock, HW_ID bits
+// 15:0 (wave slot, SIMD, CU, SH, SE) at 40, XCC_ID at 56
+#define WAVE_TS_ID(g)                                                                      \
+    do {                                                                                   \
+        const unsigned st_ = (gridDim.x + BT_BLK - 1) / BT_BLK;                            \
+        if ((threadIdx.x & 63) == 0 && (g) < BT_GENS && blockIdx.x % st_ == 0) {           \
+            const unsigned long long hw_ = __builtin_amdgcn_s_getreg((31 << 11) | 4);      \
+            const unsigned long long xc_ = __builtin_amdgcn_s_getreg((3 << 11) | 20);      \
+            hpe_blk_ts[((g) * BT_BLK + blockIdx.x / st_) * BT_PTS + (threadIdx.x >> 6)] =   \
+                (__builtin_amdgcn_s_memrealtime() & 0xFFFFFFFFFFull) | ((hw_ & 0xFFFF) << 40) | \
+                ((xc_ & 0xF) << 56);                                                       \
+        }                                                                                  \
+    } while (0)
 #else
+#define WAVE_TS_ID(g) \
+    do {              \
+    } while (0)
 #define WAVE_TS(g, k) \
     do {              \
     } while (0)
@@ -999,6 +1017,170 @@ __device__ __forceinline__ double search_align_lane(const FkSm &f, const CV &cv,
     return acc;
 }
 
+// ---------------------------------------------------------------- filter search (wave form)
+// BFMatcher's match decided from a cheap fp32 estimate of every d2, with the exact search
+// only for the points whose estimate cannot decide it.  Per particle (filt_setup): an origin
+// o (the centres' mean), s'_j = Sp_j - o, and per centre (-2 s'_j, |s'_j|^2 + 1) in LDS; per
+// point q' = (float)p - o, Q = |q'|^2 and
+//     a_j = ((|s'_j|^2 + 1) + Q) + q'.(-2 s'_j)          (one add + three fma per centre)
+// which estimates D_j + 1, D_j = |(float)p - Sp_j|^2 (real), within
+//     |a_j - (D_j + 1)| <= 11.1 u ((|q'| + |s'_j|)^2 + 1) <= 22.3 u (Q + R + 1),  u = 2^-24,
+// R = max_j |s'_j|^2 (the fp32 rounding of the estimate, 9.0 u, and of the two translations,
+// 2.01 u).  E = 64 u (Q + R + 1) bounds it with margin; E < 1/2 keeps every a_j positive, so
+// their bit patterns order like their values.  Keys (bits(a_j) & ~63) | j give, through a
+// min / second-min tree, the smallest key K1 (j* = K1 & 63) and the next K2: every other j has
+// a_j >= v2 = float(K2 & ~63), and a_j* <= v1 = float(K1 | 63).  If v2 - v1 > 2E + M,
+// M = 32 u (v1 + E), then D_j - D_j* > 23.2 u D_j* for every j != j*, so the reference's fp32
+// d2 (within 5.01 u of D) of every other centre lies above the sqrt class of d2_j* (4 ulps,
+// <= 8 u): j* is BFMatcher's match, whatever the ties in the estimate.  Otherwise (two centres
+// within the bound: ~0.06 % of points on the bench sequence), bf_search_lane decides exactly.
+// NaN or infinite inputs fail the test (comparisons with NaN are false) and go the exact way.
+struct __align__(16) FiltSm {
+    float ax[HPE_NS], ay[HPE_NS], az[HPE_NS], aw[HPE_NS];  // -2 s'_j, |s'_j|^2 + 1
+};
+struct FiltC {
+    float ox, oy, oz;  // origin
+    float K;           // R + 1
+};
+__device__ __forceinline__ float row_sum16_f32(float v) {
+    v += __int_as_float(dpp_i32<0xB1>(__float_as_int(v)));
+    v += __int_as_float(dpp_i32<0x4E>(__float_as_int(v)));
+    v += __int_as_float(dpp_i32<0x141>(__float_as_int(v)));
+    v += __int_as_float(dpp_i32<0x140>(__float_as_int(v)));
+    return v;
+}
+__device__ __forceinline__ float wave_sum_f32(float v) {
+    v = row_sum16_f32(v);
+    return ((__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)) +
+             __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16))) +
+            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32))) +
+           __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+}
+__device__ __forceinline__ float wave_max_f32(float v) {  // v >= 0 (or NaN: result unspecified)
+    v = fmaxf(v, __int_as_float(dpp_i32<0xB1>(__float_as_int(v))));
+    v = fmaxf(v, __int_as_float(dpp_i32<0x4E>(__float_as_int(v))));
+    v = fmaxf(v, __int_as_float(dpp_i32<0x141>(__float_as_int(v))));
+    v = fmaxf(v, __int_as_float(dpp_i32<0x140>(__float_as_int(v))));
+    return fmaxf(fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)),
+                       __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16))),
+                 fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)),
+                       __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48))));
+}
+// one wave, after FK: own = this lane's centre (lanes < 48).  The caller syncs the wave
+// before the search reads fs.
+__device__ __forceinline__ FiltC filt_setup(FiltSm &fs, const SphXYZ &own) {
+    const int l = threadIdx.x & 63;
+    const bool on = l < HPE_NS;
+    const float sx = (float)own.x, sy = (float)own.y, sz = (float)own.z;
+    FiltC c;
+    const float inv = 1.0f / HPE_NS;
+    c.ox = wave_sum_f32(on ? sx : 0.0f) * inv;
+    c.oy = wave_sum_f32(on ? sy : 0.0f) * inv;
+    c.oz = wave_sum_f32(on ? sz : 0.0f) * inv;
+    const float tx = sx - c.ox, ty = sy - c.oy, tz = sz - c.oz;
+    const float r2 = (tx * tx + ty * ty) + tz * tz;
+    c.K = wave_max_f32(on ? r2 : 0.0f) + 1.0f;
+    if (on) {
+        fs.ax[l] = -2.0f * tx;
+        fs.ay[l] = -2.0f * ty;
+        fs.az[l] = -2.0f * tz;
+        fs.aw[l] = r2 + 1.0f;
+    }
+    return c;
+}
+__device__ __forceinline__ unsigned med3_u32(unsigned a, unsigned b, unsigned c) {
+    unsigned r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+struct Min2 {
+    unsigned m, s;  // smallest, second smallest
+};
+__device__ __forceinline__ Min2 min2_leaf(unsigned a, unsigned b, unsigned c) {
+    return Min2{min(min(a, b), c), med3_u32(a, b, c)};
+}
+// the second smallest of the union is the smaller of the second smallest minimum and the
+// smallest second (the minimum's own group provides it, every other group's second exceeds
+// that group's minimum)
+__device__ __forceinline__ Min2 min2_merge3(Min2 a, Min2 b, Min2 c) {
+    return Min2{min(min(a.m, b.m), c.m), min(med3_u32(a.m, b.m, c.m), min(min(a.s, b.s), c.s))};
+}
+__device__ __forceinline__ Min2 min2_merge2(Min2 a, Min2 b) {
+    return Min2{min(a.m, b.m), med3_u32(a.m, b.m, min(a.s, b.s))};
+}
+template <int J0>
+__device__ __forceinline__ Min2 filt_half(const FiltSm &fs, float qx, float qy, float qz, float Q) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 q2x = {qx, qx}, q2y = {qy, qy}, q2z = {qz, qz}, q2w = {Q, Q};
+    unsigned key[24];
+#pragma unroll
+    for (int j = 0; j < 24; j += 4) {
+        const f4 ax = *(const f4 *)(fs.ax + J0 + j), ay = *(const f4 *)(fs.ay + J0 + j),
+                 az = *(const f4 *)(fs.az + J0 + j), aw = *(const f4 *)(fs.aw + J0 + j);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const f2 wx = h ? f2{ax.z, ax.w} : f2{ax.x, ax.y};
+            const f2 wy = h ? f2{ay.z, ay.w} : f2{ay.x, ay.y};
+            const f2 wz = h ? f2{az.z, az.w} : f2{az.x, az.y};
+            const f2 ww = h ? f2{aw.z, aw.w} : f2{aw.x, aw.y};
+            f2 a = ww + q2w;
+            a = __builtin_elementwise_fma(q2x, wx, a);
+            a = __builtin_elementwise_fma(q2y, wy, a);
+            a = __builtin_elementwise_fma(q2z, wz, a);
+            key[j + 2 * h] = __float_as_uint(a.x);
+            key[j + 2 * h + 1] = __float_as_uint(a.y);
+        }
+    }
+#define HPE_FKEY(J) asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(key[J]) : "v"(key[J]), "s"(0xFFFFFFC0u), "i"(J0 + J));
+    HPE_FKEY(0) HPE_FKEY(1) HPE_FKEY(2) HPE_FKEY(3) HPE_FKEY(4) HPE_FKEY(5) HPE_FKEY(6)
+    HPE_FKEY(7) HPE_FKEY(8) HPE_FKEY(9) HPE_FKEY(10) HPE_FKEY(11) HPE_FKEY(12) HPE_FKEY(13)
+    HPE_FKEY(14) HPE_FKEY(15) HPE_FKEY(16) HPE_FKEY(17) HPE_FKEY(18) HPE_FKEY(19) HPE_FKEY(20)
+    HPE_FKEY(21) HPE_FKEY(22) HPE_FKEY(23)
+#undef HPE_FKEY
+    Min2 L[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) L[k] = min2_leaf(key[3 * k], key[3 * k + 1], key[3 * k + 2]);
+    return min2_merge3(min2_merge3(L[0], L[1], L[2]), min2_merge3(L[3], L[4], L[5]),
+                       min2_merge2(L[6], L[7]));
+}
+__device__ __forceinline__ BfOut bf_filter_lane(const FkSm &f, const FiltSm &fs, const FiltC &c,
+                                                const DevHand *__restrict__ H, float qx,
+                                                float qy, float qz) {
+    const float px = qx - c.ox, py = qy - c.oy, pz = qz - c.oz;
+    const float Q = (px * px + py * py) + pz * pz;
+    const Min2 r = min2_merge2(filt_half<0>(fs, px, py, pz, Q), filt_half<24>(fs, px, py, pz, Q));
+    constexpr float U64 = 64.0f / 16777216.0f, U32 = 32.0f / 16777216.0f;
+    const float E = (Q + c.K) * U64;
+    const float v1 = __uint_as_float(r.m | 63u), v2 = __uint_as_float(r.s & ~63u);
+    const float M = (v1 + E) * U32;
+    if ((v2 - v1 > E * 2.0f + M) && (E < 0.5f)) {
+        const int ic = (int)(r.m & 63u);
+        return BfOut{ic, ic, f.S[ic][0], f.S[ic][1], f.S[ic][2], H->radii[ic]};
+    }
+    return bf_search_lane(f, H, qx, qy, qz);
+}
+// points p0, p0 + step, ... of an HBM cloud, the next one loaded one ahead; pre = that of p0
+template <class CV>
+__device__ __forceinline__ double search_align_filt(const FkSm &f, const FiltSm &fs,
+                                                    const FiltC &c, const CV &cv,
+                                                    const DevHand *__restrict__ H, Pt pre,
+                                                    int p0, int step) {
+    double acc = 0.0;
+    Pt q = pre;
+    for (int p = p0; p < cv.n; p += step) {
+        asm volatile("" ::: "memory");  // the tables re-read from LDS per point (registers)
+        const int pn = min(p + step, cv.n - 1);
+        const Pt qn = Pt{cv.cx[pn], cv.cy[pn], cv.cz[pn]};
+        const BfOut r = bf_filter_lane(f, fs, c, H, (float)q.x, (float)q.y, (float)q.z);
+        const double dx = q.x - r.cx, dy = q.y - r.cy, dz = q.z - r.cz;
+        const double e = sqrt((dx * dx + dy * dy) + dz * dz) - r.cr;
+        acc += e * e;
+        q = qn;
+    }
+    return acc;
+}
+
 // Alignment with frozen correspondences (cal_cost2(..., compute_corr=false)) over
 // `stride` lanes starting at `lane0`: per point e = |p - S[m]| - r[m], sum of e^2.
 template <class CV>
@@ -1126,19 +1308,35 @@ __device__ __forceinline__ double align_frozen_pts(const FkSm &f, const FrozenPt
 #endif
 enum EvalMode { EV_COST = 0, EV_COST2_CORR = 1, EV_COST2_FROZEN = 2, EV_COST_STORE = 3 };
 
-// cal_cost of the particle in f.th by ONE wave (FK + search over 64 lanes): the
-// throughput form used when there are many more particles than CUs.  All lanes return
-// the total; pre = load_pt1(cv, lane).
-template <class CV>
-__device__ __forceinline__ double eval_wave_cost(FkSm &f, const DevObs &o, const CV &cv,
-                                                 const DevHand *__restrict__ H, Pt pre) {
+// cal_cost of the particle in f.th by WPP waves of one workgroup (the throughput form used
+// when there are many more particles than CUs): each wave runs FK on its own workspace (the
+// same operations on the same inputs: the same bits) and searches points l + 64 sub,
+// l + 64 (sub + WPP), ...; sub 0 adds the depth terms.  WPP = 2 (swarms of at most one
+// particle per SIMD) halves the search's latency; the wave totals are added in sub order
+// through xpart (indexed by wave) behind a workgroup barrier that every wave reaches.
+// All lanes of the particle's waves return the total; pre = load_pt1(cv, l + 64 sub).
+template <int WPP, class CV>
+__device__ __forceinline__ double eval_wave_cost(FkSm &f, FiltSm &fs, const DevObs &o,
+                                                 const CV &cv, const DevHand *__restrict__ H,
+                                                 Pt pre, int sub, double *xpart,
+                                                 int g_ts = BT_GENS) {
     const int l = threadIdx.x & 63;
     SphXYZ own;
     fk_wave(f, H, &own);
     const DepthG dg = depth_issue_at(own, l, o, H);
-    double al = search_align_lane(f, cv, H, pre);
-    double dep = depth_finish(dg, o, l < HPE_NS);
-    return wave_sum(al * o.lambda + dep);
+    const FiltC fc = filt_setup(fs, own);
+    wave_sync();
+    WAVE_TS(g_ts, 8);
+    double al = search_align_filt(f, fs, fc, cv, H, pre, l + 64 * sub, 64 * WPP);
+    if (HPE_STAMPS) asm volatile("" ::"v"(al));
+    WAVE_TS(g_ts, 12);
+    double dep = depth_finish(dg, o, l < HPE_NS && sub == 0);
+    const double part = wave_sum(al * o.lambda + dep);
+    if (WPP == 1) return part;
+    const int w = threadIdx.x >> 6;
+    if (l == 0) xpart[w] = part;
+    __syncthreads();
+    return xpart[w - sub] + xpart[w - sub + 1];
 }
 
 __device__ __forceinline__ CloudGlobal obs_cloud(const DevObs &o) {

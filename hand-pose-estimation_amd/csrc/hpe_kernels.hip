@@ -602,14 +602,17 @@ __device__ __forceinline__ void push_inbox_w(const DevSwarm &sw, int g, int s, i
     }
 }
 
+template <int WPP>
 __global__ __launch_bounds__(PW_NT) void k_pso_init_w(DevSwarm sw, const double *__restrict__ x0,
                                                       const DevObs *__restrict__ og,
                                                       const DevHand *__restrict__ Hg) {
     const DevObs o = *og;
     __shared__ DevHand hs;
     __shared__ FkSm fks[PW_WPB];
-    const int t = threadIdx.x, w = t >> 6, l = t & 63;
-    const int i = blockIdx.x * PW_WPB + w, P = sw.P;
+    __shared__ FiltSm fls[PW_WPB];
+    __shared__ double xpart[PW_WPB];
+    const int t = threadIdx.x, w = t >> 6, l = t & 63, sub = w % WPP;
+    const int i = blockIdx.x * (PW_WPB / WPP) + w / WPP, P = sw.P;
     const bool valid = i < P;
     const int ic = valid ? i : P - 1;
     const double hw = hand_word<PW_NT>(Hg);
@@ -618,14 +621,14 @@ __global__ __launch_bounds__(PW_NT) void k_pso_init_w(DevSwarm sw, const double 
     Link lk[3];
     push_lane_links(sw, 0, ic, l, 1, -1, lk);
     const CloudGlobal cv = obs_cloud(o);
-    const Pt pre = load_pt1(cv, l);
+    const Pt pre = load_pt1(cv, l + 64 * sub);
     const double *sd = sw.bounds + 2 * HPE_DOF;
     if (sw.ext && blockIdx.x == 0 && t == 0) sw.ext[HPE_DOF] = __builtin_inf();  // no candidate yet
     if (l < HPE_DOF) {  // particles = x0 + randn % std (PSO.cpp:67-72)
         const size_t e = (size_t)ic * HPE_DOF + l;
         const double x = x0[l] + sw.normals[e] * sd[l];
         f.th[l] = x;
-        if (valid) {
+        if (valid && sub == 0) {
             sw.xh[e] = x;
             sw.pb[e] = x;
             sw.v[e] = 0.0;
@@ -633,8 +636,8 @@ __global__ __launch_bounds__(PW_NT) void k_pso_init_w(DevSwarm sw, const double 
     }
     hand_put<PW_NT>(hs, hw);
     __syncthreads();  // hand staged
-    const double c = eval_wave_cost(f, o, cv, H, pre);
-    if (!valid) return;
+    const double c = eval_wave_cost<WPP>(f, fls[w], o, cv, H, pre, sub, xpart);
+    if (!valid || sub != 0) return;
     if (l == 0) {
         sw.pch[i] = c;
         gmin_lower(sw, 0, i, c);
@@ -643,7 +646,7 @@ __global__ __launch_bounds__(PW_NT) void k_pso_init_w(DevSwarm sw, const double 
     for (int k = 0; k < 3; ++k) push_inbox_w(sw, 0, i, l + 64 * k, lk[k], 1, c, f.th);
 }
 
-template <bool XCH, bool ROW16>
+template <bool XCH, bool ROW16, int WPP>
 __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *__restrict__ og,
                                                      const DevHand *__restrict__ Hg, int g,
                                                      double W1, double C1, double C2) {
@@ -653,20 +656,22 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
         "s"(sw.xh), "s"(sw.pch), "s"(sw.pb), "s"(sw.v), "s"(sw.inbox), "s"(sw.ibtc),
         "s"(sw.P), "s"(sw.K));
     const DevObs o = *og;
+    WAVE_TS_ID(g);
     __shared__ DevHand hs;
     __shared__ FkSm fks[PW_WPB];
-    const int t = threadIdx.x + z0, w = t >> 6, l = t & 63;
-    const int i = blockIdx.x * PW_WPB + w, P = sw.P, K = sw.K;
+    __shared__ FiltSm fls[PW_WPB];
+    __shared__ double xpart[PW_WPB];
+    const int t = threadIdx.x + z0, w = t >> 6, l = t & 63, sub = w % WPP;
+    const int i = blockIdx.x * (PW_WPB / WPP) + w / WPP, P = sw.P, K = sw.K;
     const bool valid = i < P;
     const int ic = valid ? i : P - 1;
     const double hw = hand_word<PW_NT>(Hg);  // staged into LDS before the block barrier
     const DevHand *__restrict__ H = &hs;
     FkSm &f = fks[w];
-    // ---- round 1: every load of the generation, all independent and unconditional
-    // (the push links are loaded after the evaluation: held across it they would take the
-    // registers of a third wave per SIMD; the other waves hide that load)
+    // ---- round 1: every load of the generation, all independent and unconditional (the
+    // push links follow once the topology is known)
     const CloudGlobal cv = obs_cloud(o);
-    const Pt pre = load_pt1(cv, l);
+    const Pt pre = load_pt1(cv, l + 64 * sub);
     const size_t e = (size_t)ic * HPE_DOF + l;
     const size_t ec = (size_t)ic * HPE_DOF + (l < HPE_DOF ? l : HPE_DOF - 1);
     const double xo = sw.xh[(size_t)(g - 1) * P * HPE_DOF + ec];
@@ -687,9 +692,12 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
     const Sig pv = sw.sig[g > 1 ? g - 1 : 0];
     const double exr = XCH ? sw.ext[l <= HPE_DOF ? l : HPE_DOF] : 0.0;  // exchange (sw.ext)
     // the draws while the loads are in flight
-    const int dl = l < HPE_DOF ? l : 0;
-    const double rp = philox_u01(sw.seed, ST_RP, g, ic, dl);
-    const double rg = philox_u01(sw.seed, ST_RG, g, ic, dl);
+    // one Philox pass for both draws: lanes 0..25 draw rp of dimension l, lanes 26..51 rg of
+    // dimension l - 26, which one shuffle brings to lane l - 26
+    const int dl = l < HPE_DOF ? l : (l < 2 * HPE_DOF ? l - HPE_DOF : 0);
+    const double rd = philox_u01(sw.seed, l < HPE_DOF ? ST_RP : ST_RG, g, ic, dl);
+    const double rp = rd;
+    const double rg = __shfl(rd, l + HPE_DOF);
     const double fmin = gmin_reduce(gcell);
     // ---- end-of-generation update of g-1 (PSO.cpp:864-877), uniform
     Sig sg;
@@ -704,7 +712,7 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
         sg.topo = pv.topo;
     }
     if (sg.count > 0) sg.topo = g;
-    if (i == 0 && l == 0) sw.sig[g] = sg;
+    if (i == 0 && l == 0 && sub == 0) sw.sig[g] = sg;
     const int topo = sg.topo, var = (topo == g) ? 1 : 0;
     // ---- informant (PSO.cpp:810-812)
     const int self_lane = ROW16 ? 15 : 63;  // one 16-lane row when K <= 15
@@ -740,17 +748,23 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
         const double xr = xn;
         if (xr < lbt) { xn = lbt; vn = 0.; }
         if (xr > ubt) { xn = lbt; vn = 0.; }  // above max -> MIN (PSO.cpp:372)
-        if (valid) {
+        if (valid && sub == 0) {
             sw.v[e] = vn;
             sw.xh[(size_t)g * P * HPE_DOF + e] = xn;
         }
         f.th[l] = xn;
     }
+    // the push links, loaded before the evaluation so their round trip hides under it (121 ->
+    // 127 VGPRs: still four waves per SIMD)
+    Link lk[3];
+    push_lane_links(sw, g, ic, l, g + 1, topo, lk);
     hand_put<PW_NT>(hs, hw);
+    WAVE_TS(g, 4);
     __syncthreads();  // hand staged (the only block-wide sync)
     // ---- evaluation and pbest (PSO.cpp:848-861)
-    const double fx = eval_wave_cost(f, o, cv, H, pre);
-    if (!valid) return;
+    const double fx = eval_wave_cost<WPP>(f, fls[w], o, cv, H, pre, sub, xpart, g);
+    WAVE_TS(g, 16);
+    if (!valid || sub != 0) return;
     const bool better = fx < pci;
     const double pn = better ? fx : pci;
     if (l < HPE_DOF) {
@@ -758,8 +772,6 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
         sw.pb[e] = row;
         f.th[l] = row;
     }
-    Link lk[3];
-    push_lane_links(sw, g, ic, l, g + 1, topo, lk);
     if (l == 0) {
         sw.pch[(size_t)g * P + i] = pn;
         gmin_lower(sw, g, i, pn);
@@ -770,6 +782,7 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
         const int q = l + 64 * k;
         push_inbox_w(sw, g, i, q, lk[k], q < 3 * IB_FIELDS ? g + 1 : topo, pn, f.th);
     }
+    WAVE_TS(g, 20);
 }
 
 // The opt-in per-generation exchange (hpe_set_exchange): this subswarm's best after

@@ -407,12 +407,16 @@ def test_edge_empty_frame_optimisers(oracle, ora_hand, gpu_hand):
     assert pso.last_gbest_cost == oc
 
 
-@pytest.mark.parametrize("P,maxiter", [(32, 11), (7, 4), (1, 3), (1030, 3)])
-def test_pso_evolve_wave_form(oracle, ora_hand, np_hand, P, maxiter, monkeypatch):
-    """The one-wave-per-particle generation kernels (used for large swarms) against the
-    oracle, including a ragged last workgroup (P not a multiple of 4)."""
+@pytest.mark.parametrize("P,maxiter,wpp", [(32, 11, 0), (7, 4, 0), (1, 3, 0), (1030, 3, 0),
+                                           (32, 11, 1), (1030, 3, 2), (7, 4, 2)])
+def test_pso_evolve_wave_form(oracle, ora_hand, np_hand, P, maxiter, wpp, monkeypatch):
+    """The wave-form generation kernels (used for large swarms) against the oracle,
+    including a ragged last workgroup (P not a multiple of the particles per workgroup), with
+    one or two waves per particle (wpp 0: the context's choice, two up to 1024 particles)."""
     import hpe
     monkeypatch.setenv("HPE_PSO_FORM", "wave")
+    if wpp:
+        monkeypatch.setenv("HPE_PSO_WPP", str(wpp))
     gh = hpe.reference_hand(device=0)  # context created with the wave form forced
     truth = hand_data.trajectory(2, seed=9)[1]
     d = oracle_np.render_depth_mm(np_hand, truth)
@@ -430,6 +434,48 @@ def test_pso_evolve_wave_form(oracle, ora_hand, np_hand, P, maxiter, monkeypatch
     g, cnt, topo = pso.trace(cf)
     np.testing.assert_allclose(g, tr["gbest"], rtol=1e-8)
     assert np.array_equal(cnt, tr["count"]) and np.array_equal(topo, tr["topo"])
+
+
+@pytest.mark.parametrize("n_ties", [400, 4000])
+def test_wave_form_filter_search_ties(oracle, ora_hand, n_ties, monkeypatch):
+    """The wave form's filter search (hpe_device.hpp bf_filter_lane) on points that defeat
+    its estimate: float midpoints of centre pairs (exact and near ties, decided by the exact
+    search) and the centres themselves (d2 = 0), with a swarm whose particles all sit at the
+    pose the cloud was built from (std 0): every evaluation of both wave-form kernels (init and
+    one generation) must equal the oracle's cal_cost, whose match takes the first of equal
+    distances.  A wrong pick changes the alignment term (the radii differ)."""
+    import hpe
+    import oracle_c
+    monkeypatch.setenv("HPE_PSO_FORM", "wave")
+    gh = hpe.reference_hand(device=0)
+    th = oracle_np.X0
+    S = oracle.build(ora_hand, th).astype(np.float32).astype(np.float64)
+    rng = np.random.default_rng(4)
+    pts = []
+    for _ in range(n_ties):
+        a, b = rng.choice(48, 2, replace=False)
+        pts.append(0.5 * (S[a] + S[b]))
+    pts += list(S)
+    cloud = np.array(pts)
+    depth = np.zeros((240, 320)); dt = np.zeros((240, 320), np.float32)
+    K = np.array([[241.42, 0, 160], [0, 241.42, 120], [0, 0, 1.0]])
+    obs = oracle_c.Obs(depth, dt, cloud, 0.1, 0.0, K)
+    gh.ctx.store_frame(3, depth, dt, cloud, 0.1, 0.0, K)
+    gh.ctx.select_frame(3)
+    gh.ctx.frame_token = None
+    om = hpe.observedmodel(); om._obs = dict(cloud=cloud); om.token = -1
+    cf = hpe.costfunc(gh, om)
+    cf._sync_frame = lambda: None
+    ub, lb, _ = oracle_np.reference_bounds()
+    pso = hpe.PSO()
+    pso.set_pso_params(ub, lb, np.zeros(26), 0.7298, 1.49618, 1.49618, 2, 1e-8, 1e-8)
+    bestp = np.zeros(26)
+    assert pso.pso_evolve(cf, th.copy(), 1024, bestp) == 1
+    ref = oracle.cal_cost(ora_hand, obs, th)
+    assert abs(pso.last_gbest_cost - ref) <= RTOL * abs(ref)
+    g, _, _ = pso.trace(cf)
+    np.testing.assert_allclose(g, ref, rtol=RTOL)
+    np.testing.assert_array_equal(bestp, th)
 
 
 @pytest.mark.parametrize("P,maxiter", [(1024, 4), (1030, 3)])
