@@ -16,10 +16,12 @@ for p in (ROOT, PKG, ROOT / "oracle", ROOT / "tests"):
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a gfx950 GPU (run with -m gpu)")
-    mark = config.getoption("-m") or ""
-    if "gpu" in mark and "not gpu" not in mark:
-        # torch's HIP runtime must initialise before libhpe.so's (tests that hand torch
-        # device buffers to the ABI)
+
+
+def pytest_collection_modifyitems(config, items):
+    # torch's HIP runtime must initialise before libhpe.so's (tests that hand torch device
+    # buffers to the ABI): whenever a selected test is a GPU test, however it was selected
+    if any(it.get_closest_marker("gpu") for it in items):
         import torch
         torch.cuda.is_available()
 
