@@ -409,6 +409,103 @@ __device__ __forceinline__ void fk_wave_t(FkSm &f, const DevHand *__restrict__ H
     sc.lap(14);
 }
 
+// FK of NP particles by the whole workgroup (the wave form, round 5): the three phases of fk_wave_t with their items spread over the workgroup's
+// threads instead of each wave running its own particle's phases on 23, 15 and 48 of its
+// lanes -- trig on NP x 23 threads, chain rows on NP x 15, spheres on NP x 48 -- with a
+// workgroup barrier after each.  The per-item operations are fk_wave_t's (FK_FULL, inline
+// trig), so the centres are the same bits; fk[p * STRIDE] is particle p's workspace (STRIDE:
+// waves per particle).  Every thread of the workgroup calls it.
+template <int NP, int STRIDE>
+__device__ __forceinline__ void fk_coop(FkSm *fk, const DevHand *__restrict__ H) {
+    const int t = threadIdx.x;
+    // this thread's chain row and sphere item, their hand constants loaded first
+    const int pc = min(t / 15, NP - 1), l = t - 15 * (t / 15);
+    const int dl = (t < NP * 15) ? l / 3 : 0;
+    const double L2 = H->L[dl][2], L3 = H->L[dl][3];
+    const double Fc = H->Fc[dl], Fs = H->Fs[dl], FLc = H->FLc[dl], FLs = H->FLs[dl];
+    const double T10x = H->T10x[dl], T10y = H->T10y[dl];
+    const double L1 = H->L[dl][1], tc = H->twc[dl], ts = H->tws[dl];
+    const int ps = min(t / HPE_NS, NP - 1), sl = (t < NP * HPE_NS) ? t - HPE_NS * (t / HPE_NS) : HPE_NS - 1;
+    const int sd = H->dg[sl], sa = H->ja[sl];
+    const double swa = H->wa[sl], swb = H->wb[sl];
+    if (t < NP * 23) {  // trig: slot k of particle t / 23 (fk_wave_t phase 1)
+        const int pt = t / 23, k = t - 23 * pt;
+        FkSm &f = fk[pt * STRIDE];
+        const double th = f.th[k < 3 ? k : 6 + (k - 3)];
+        const double a = deg2rad(k == 0 ? th + 180 : th);
+        double sn, cs;
+        sincos(a, &sn, &cs);
+        f.sn[k] = sn;
+        f.cs[k] = cs;
+    }
+    __syncthreads();
+    if (t < NP * 15) {  // chain row r of digit d of particle pc (fk_wave_t phase 2, FK_FULL)
+        FkSm &f = fk[pc * STRIDE];
+        const int d = l / 3, r = l - 3 * (l / 3);
+        const double u = f.th[3 + r];
+        const double c1 = f.cs[3 + 4 * d], s1 = f.sn[3 + 4 * d];
+        const double c2 = f.cs[4 + 4 * d], s2 = f.sn[4 + 4 * d];
+        const double c3 = f.cs[5 + 4 * d], s3 = f.sn[5 + 4 * d];
+        const double c4 = f.cs[6 + 4 * d], s4 = f.sn[6 + 4 * d];
+        const double b01 = -s2 * tc, b11 = c2 * tc, L1c2 = L1 * c2, L1s2 = L1 * s2;
+        const double AB00 = c1 * c2, AB10 = s1 * c2, AB20 = -s2;
+        const double AB01 = c1 * b01 + (-s1) * ts, AB11 = s1 * b01 + c1 * ts, AB21 = -b11;
+        const double AB03 = c1 * L1c2, AB13 = s1 * L1c2, AB23 = -L1s2;
+        const double cz = f.cs[0], sz = f.sn[0], cy = f.cs[1], sy = f.sn[1];
+        const double cxr = f.cs[2], sxr = f.sn[2];
+        double z0, z1, z2;
+        if (r == 0) { z0 = cz; z1 = -sz; z2 = 0; }
+        else if (r == 1) { z0 = sz; z1 = cz; z2 = 0; }
+        else { z0 = 0; z1 = 0; z2 = 1; }
+        const double q0 = z0 * cy + z2 * (-sy);
+        const double q1 = z1;
+        const double q2 = z0 * sy + z2 * cy;
+        const double g0 = q0;
+        const double g1 = q1 * cxr + q2 * sxr;
+        const double g2 = q1 * (-sxr) + q2 * cxr;
+        const double h0 = g0 * Fc + g1 * Fs;
+        const double h1 = g0 * (-Fs) + g1 * Fc;
+        const double h2 = g2;
+        const double X1 = g0 * FLc + g1 * FLs;
+        const double X0 = h0 * T10x + h1 * T10y;
+        const double k0 = (h0 * AB00 + h1 * AB10) + h2 * AB20;
+        const double k1 = (h0 * AB01 + h1 * AB11) + h2 * AB21;
+        const double X2 = (h0 * AB03 + h1 * AB13) + h2 * AB23;
+        const double m0 = k0 * c3 + k1 * s3;
+        const double m1 = k0 * (-s3) + k1 * c3;
+        const double X3 = k0 * (L2 * c3) + k1 * (L2 * s3);
+        const double X4 = m0 * (L3 * c4) + m1 * (L3 * s4);
+        const double J1 = X1 + u;
+        const double J0 = X0 + J1;
+        const double J2 = X2 + J1;
+        const double J3 = X3 + J2;
+        const double J4 = X4 + J3;
+        f.J[d][0][r] = J0;
+        f.J[d][1][r] = J1;
+        f.J[d][2][r] = J2;
+        f.J[d][3][r] = J3;
+        f.J[d][4][r] = J4;
+    }
+    __syncthreads();
+    if (t < NP * HPE_NS) {  // sphere sl of particle ps (fk_wave_t phase 3)
+        FkSm &f = fk[ps * STRIDE];
+        double ja[3], jb[3];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            ja[r] = f.J[sd][sa][r];
+            jb[r] = f.J[sd][sa + 1][r];
+        }
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            const double v = swa * ja[r] + swb * jb[r];
+            const double vs = (r == 0) ? v : v * -1;
+            f.S[sl][r] = vs;
+            f.Sp[r][sl] = (float)vs;
+        }
+    }
+    __syncthreads();
+}
+
 template <bool OUTLINE_TRIG = false>
 __device__ __forceinline__ void fk_wave(FkSm &f, const DevHand *__restrict__ H,
                                         SphXYZ *own = nullptr, const double *thr = nullptr) {
@@ -1315,14 +1412,25 @@ enum EvalMode { EV_COST = 0, EV_COST2_CORR = 1, EV_COST2_FROZEN = 2, EV_COST_STO
 // particle per SIMD) halves the search's latency; the wave totals are added in sub order
 // through xpart (indexed by wave) behind a workgroup barrier that every wave reaches.
 // All lanes of the particle's waves return the total; pre = load_pt1(cv, l + 64 sub).
-template <int WPP, class CV>
-__device__ __forceinline__ double eval_wave_cost(FkSm &f, FiltSm &fs, const DevObs &o,
+// COOP: FK by the whole workgroup (fk_coop over its NPW / WPP particles, particle p's
+// centres in fks[p * WPP], read by all its waves); otherwise each wave runs its own (fk_wave
+// on fks[w]).
+template <int WPP, bool COOP, int NPW, class CV>
+__device__ __forceinline__ double eval_wave_cost(FkSm *fks, FiltSm &fs, const DevObs &o,
                                                  const CV &cv, const DevHand *__restrict__ H,
                                                  Pt pre, int sub, double *xpart,
                                                  int g_ts = BT_GENS) {
     const int l = threadIdx.x & 63;
+    FkSm &f = fks[COOP ? (threadIdx.x >> 6) - sub : (threadIdx.x >> 6)];
     SphXYZ own;
-    fk_wave(f, H, &own);
+    if (COOP) {
+        fk_coop<NPW / WPP, WPP>(fks, H);
+        const int sl = l < HPE_NS ? l : HPE_NS - 1;
+        own = SphXYZ{f.S[sl][0], f.S[sl][1], f.S[sl][2]};
+        if (l >= HPE_NS) own = SphXYZ{0.0, 0.0, 0.0};
+    } else {
+        fk_wave(f, H, &own);
+    }
     const DepthG dg = depth_issue_at(own, l, o, H);
     const FiltC fc = filt_setup(fs, own);
     wave_sync();
@@ -1510,8 +1618,13 @@ __device__ __forceinline__ double philox_u01(uint64_t seed, uint32_t stream, uin
             k0 += 0x9E3779B9u;
             k1 += 0xBB67AE85u;
         }
-        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
-        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+        // each 32 x 32 -> 64 product as ONE v_mad_u64_u32 (the compiler emits a mul_lo /
+        // mul_hi pair: two quarter-rate instructions for one)
+        uint64_t p0, p1;
+        asm("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(p0) : "s"(0xD2511F53u), "v"(c0) : "vcc");
+        asm("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(p1) : "s"(0xCD9E8D57u), "v"(c2) : "vcc");
+        const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+        const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
         const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
         c0 = n0;
         c1 = lo1;

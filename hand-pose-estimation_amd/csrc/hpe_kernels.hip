@@ -602,7 +602,7 @@ __device__ __forceinline__ void push_inbox_w(const DevSwarm &sw, int g, int s, i
     }
 }
 
-template <int WPP>
+template <int WPP, bool COOP>
 __global__ __launch_bounds__(PW_NT) void k_pso_init_w(DevSwarm sw, const double *__restrict__ x0,
                                                       const DevObs *__restrict__ og,
                                                       const DevHand *__restrict__ Hg) {
@@ -636,7 +636,7 @@ __global__ __launch_bounds__(PW_NT) void k_pso_init_w(DevSwarm sw, const double 
     }
     hand_put<PW_NT>(hs, hw);
     __syncthreads();  // hand staged
-    const double c = eval_wave_cost<WPP>(f, fls[w], o, cv, H, pre, sub, xpart);
+    const double c = eval_wave_cost<WPP, COOP, PW_WPB>(fks, fls[w], o, cv, H, pre, sub, xpart);
     if (!valid || sub != 0) return;
     if (l == 0) {
         sw.pch[i] = c;
@@ -646,8 +646,10 @@ __global__ __launch_bounds__(PW_NT) void k_pso_init_w(DevSwarm sw, const double 
     for (int k = 0; k < 3; ++k) push_inbox_w(sw, 0, i, l + 64 * k, lk[k], 1, c, f.th);
 }
 
-template <bool XCH, bool ROW16, int WPP>
-__global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *__restrict__ og,
+// one wave per particle: four waves per SIMD, so every workgroup of a 4096 swarm is
+// resident (the register count sits at the 128 boundary)
+template <bool XCH, bool ROW16, int WPP, bool COOP>
+__global__ __launch_bounds__(PW_NT, WPP == 1 ? 4 : 2) void k_pso_gen_w(DevSwarm sw, const DevObs *__restrict__ og,
                                                      const DevHand *__restrict__ Hg, int g,
                                                      double W1, double C1, double C2) {
     // every argument word loaded at entry in one batch (see k_pso_gen)
@@ -762,7 +764,7 @@ __global__ __launch_bounds__(PW_NT) void k_pso_gen_w(DevSwarm sw, const DevObs *
     WAVE_TS(g, 4);
     __syncthreads();  // hand staged (the only block-wide sync)
     // ---- evaluation and pbest (PSO.cpp:848-861)
-    const double fx = eval_wave_cost<WPP>(f, fls[w], o, cv, H, pre, sub, xpart, g);
+    const double fx = eval_wave_cost<WPP, COOP, PW_WPB>(fks, fls[w], o, cv, H, pre, sub, xpart, g);
     WAVE_TS(g, 16);
     if (!valid || sub != 0) return;
     const bool better = fx < pci;

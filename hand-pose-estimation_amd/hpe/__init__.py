@@ -82,7 +82,13 @@ class Context:
     @property
     def refine_exact(self) -> bool:
         """True: refine_init_pose places spheres by the reference's DH chain on every
-        evaluation; False (default): the hand-frame form (hpe_set_refine_exact)."""
+        evaluation; False (default): the hand-frame form (hpe_set_refine_exact).
+
+        The two forms differ in fp64 operation order only (centres within 1e-12 cm).  Over
+        the 400-frame sequence test the default form's refine took a different number of
+        evaluations than the reference-order oracle on 6 frames, each a replayed near-tie
+        (relative margin < 1e-13), and the tracked poses stayed within 2.2e-7 per frame and
+        2.8e-7 of the free-running reference-order oracle."""
         return bool(self.lib.hpe_get_refine_exact(self.h))
 
     @refine_exact.setter

@@ -436,6 +436,37 @@ def test_pso_evolve_wave_form(oracle, ora_hand, np_hand, P, maxiter, wpp, monkey
     assert np.array_equal(cnt, tr["count"]) and np.array_equal(topo, tr["topo"])
 
 
+@pytest.mark.parametrize("wpp", [1, 2])
+def test_wave_form_cooperative_fk_bit_identical(oracle, ora_hand, np_hand, wpp, monkeypatch):
+    """The wave form's workgroup-cooperative FK (fk_coop, the default) against each wave's
+    own FK (HPE_FK_COOP=0), at one and two waves per particle: the same operations per item,
+    so the same pose, cost and traces bit for bit (and both against the oracle)."""
+    import hpe
+    monkeypatch.setenv("HPE_PSO_FORM", "wave")
+    monkeypatch.setenv("HPE_PSO_WPP", str(wpp))
+    truth = hand_data.trajectory(2, seed=11)[1]
+    d = oracle_np.render_depth_mm(np_hand, truth)
+    ub, lb, sd = oracle_np.reference_bounds()
+    out = {}
+    for coop in ("1", "0"):
+        monkeypatch.setenv("HPE_FK_COOP", coop)
+        gh = hpe.reference_hand(device=0)
+        obs, om = _obs_pair(oracle, gh, d)
+        cf = hpe.costfunc(gh, om)
+        pso = hpe.PSO()
+        pso.set_pso_params(ub, lb, sd, 0.7298, 1.49618, 1.49618, 4, 1e-8, 1e-8)
+        bestp = np.zeros(26)
+        assert pso.pso_evolve(cf, oracle_np.X0.copy(), 1030, bestp) == 1
+        out[coop] = (bestp.copy(), pso.last_gbest_cost, pso.trace(cf))
+    assert np.array_equal(out["1"][0], out["0"][0])
+    assert out["1"][1] == out["0"][1]
+    for a, b in zip(out["1"][2], out["0"][2]):
+        assert np.array_equal(a, b)
+    rb, rc, _ = oracle.pso_evolve(ora_hand, obs, oracle_np.X0.copy(), 1030, 4, lb, ub, sd, seed=1000)
+    np.testing.assert_allclose(out["1"][0], rb, rtol=0, atol=1e-6)
+    assert abs(out["1"][1] - rc) <= 1e-8 * abs(rc)
+
+
 @pytest.mark.parametrize("n_ties", [400, 4000])
 def test_wave_form_filter_search_ties(oracle, ora_hand, n_ties, monkeypatch):
     """The wave form's filter search (hpe_device.hpp bf_filter_lane) on points that defeat
