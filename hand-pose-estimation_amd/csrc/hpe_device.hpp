@@ -1408,8 +1408,8 @@ enum EvalMode { EV_COST = 0, EV_COST2_CORR = 1, EV_COST2_FROZEN = 2, EV_COST_STO
 // cal_cost of the particle in f.th by WPP waves of one workgroup (the throughput form used
 // when there are many more particles than CUs): each wave runs FK on its own workspace (the
 // same operations on the same inputs: the same bits) and searches points l + 64 sub,
-// l + 64 (sub + WPP), ...; sub 0 adds the depth terms.  WPP = 2 (swarms of at most one
-// particle per SIMD) halves the search's latency; the wave totals are added in sub order
+// l + 64 (sub + WPP), ...; sub 0 adds the depth terms.  WPP = 2 or 4 (swarms of at most one
+// particle per SIMD) cuts the search's latency; the wave totals are added in sub order
 // through xpart (indexed by wave) behind a workgroup barrier that every wave reaches.
 // All lanes of the particle's waves return the total; pre = load_pt1(cv, l + 64 sub).
 // COOP: FK by the whole workgroup (fk_coop over its NPW / WPP particles, particle p's
@@ -1444,7 +1444,10 @@ __device__ __forceinline__ double eval_wave_cost(FkSm *fks, FiltSm &fs, const De
     const int w = threadIdx.x >> 6;
     if (l == 0) xpart[w] = part;
     __syncthreads();
-    return xpart[w - sub] + xpart[w - sub + 1];
+    double tot = xpart[w - sub];
+#pragma unroll
+    for (int k = 1; k < WPP; ++k) tot += xpart[w - sub + k];
+    return tot;
 }
 
 __device__ __forceinline__ CloudGlobal obs_cloud(const DevObs &o) {

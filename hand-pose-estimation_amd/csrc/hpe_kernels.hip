@@ -646,10 +646,10 @@ __global__ __launch_bounds__(PW_NT) void k_pso_init_w(DevSwarm sw, const double 
     for (int k = 0; k < 3; ++k) push_inbox_w(sw, 0, i, l + 64 * k, lk[k], 1, c, f.th);
 }
 
-// one wave per particle: four waves per SIMD, so every workgroup of a 4096 swarm is
+// one (four) waves per particle: four waves per SIMD, so every workgroup of a 4096 (1024) swarm is
 // resident (the register count sits at the 128 boundary)
 template <bool XCH, bool ROW16, int WPP, bool COOP>
-__global__ __launch_bounds__(PW_NT, WPP == 1 ? 4 : 2) void k_pso_gen_w(DevSwarm sw, const DevObs *__restrict__ og,
+__global__ __launch_bounds__(PW_NT, WPP == 2 ? 2 : 4) void k_pso_gen_w(DevSwarm sw, const DevObs *__restrict__ og,
                                                      const DevHand *__restrict__ Hg, int g,
                                                      double W1, double C1, double C2) {
     // every argument word loaded at entry in one batch (see k_pso_gen)
@@ -670,6 +670,17 @@ __global__ __launch_bounds__(PW_NT, WPP == 1 ? 4 : 2) void k_pso_gen_w(DevSwarm 
     const double hw = hand_word<PW_NT>(Hg);  // staged into LDS before the block barrier
     const DevHand *__restrict__ H = &hs;
     FkSm &f = fks[w];
+    // a helper wave (WPP > 1, cooperative FK): its particle's FK and state are the first
+    // wave's, so it only stages its share of the hand, takes part in the FK and searches its
+    // share of the cloud (the same barriers as the first wave's path)
+    if (COOP && WPP > 1 && __builtin_amdgcn_readfirstlane(sub) != 0) {
+        const CloudGlobal cv = obs_cloud(o);
+        const Pt pre = load_pt1(cv, l + 64 * sub);
+        hand_put<PW_NT>(hs, hw);
+        __syncthreads();
+        eval_wave_cost<WPP, COOP, PW_WPB>(fks, fls[w], o, cv, H, pre, sub, xpart, g);
+        return;
+    }
     // ---- round 1: every load of the generation, all independent and unconditional (the
     // push links follow once the topology is known)
     const CloudGlobal cv = obs_cloud(o);

@@ -408,11 +408,12 @@ def test_edge_empty_frame_optimisers(oracle, ora_hand, gpu_hand):
 
 
 @pytest.mark.parametrize("P,maxiter,wpp", [(32, 11, 0), (7, 4, 0), (1, 3, 0), (1030, 3, 0),
-                                           (32, 11, 1), (1030, 3, 2), (7, 4, 2)])
+                                           (32, 11, 1), (1030, 3, 2), (7, 4, 2), (7, 4, 4),
+                                           (1030, 3, 4)])
 def test_pso_evolve_wave_form(oracle, ora_hand, np_hand, P, maxiter, wpp, monkeypatch):
     """The wave-form generation kernels (used for large swarms) against the oracle,
     including a ragged last workgroup (P not a multiple of the particles per workgroup), with
-    one or two waves per particle (wpp 0: the context's choice, two up to 1024 particles)."""
+    one, two or four waves per particle (wpp 0: the context's choice)."""
     import hpe
     monkeypatch.setenv("HPE_PSO_FORM", "wave")
     if wpp:
@@ -436,7 +437,7 @@ def test_pso_evolve_wave_form(oracle, ora_hand, np_hand, P, maxiter, wpp, monkey
     assert np.array_equal(cnt, tr["count"]) and np.array_equal(topo, tr["topo"])
 
 
-@pytest.mark.parametrize("wpp", [1, 2])
+@pytest.mark.parametrize("wpp", [1, 2, 4])
 def test_wave_form_cooperative_fk_bit_identical(oracle, ora_hand, np_hand, wpp, monkeypatch):
     """The wave form's workgroup-cooperative FK (fk_coop, the default) against each wave's
     own FK (HPE_FK_COOP=0), at one and two waves per particle: the same operations per item,
