@@ -67,7 +67,19 @@ __device__ unsigned long long hpe_blk_ts[BT_GENS * BT_BLK * BT_PTS];
                 ((xc_ & 0xF) << 56);                                                       \
         }                                                                                  \
     } while (0)
+// finer points (k < 12) of the even waves of every sampled workgroup: slot 2 k + wave / 2
+#define WAVE_TS2(g, k)                                                                     \
+    do {                                                                                   \
+        const unsigned st_ = (gridDim.x + BT_BLK - 1) / BT_BLK;                            \
+        if ((threadIdx.x & 64) == 0 && (threadIdx.x & 63) == 0 && (g) < BT_GENS &&          \
+            blockIdx.x % st_ == 0)                                                         \
+            hpe_blk_ts[((g) * BT_BLK + blockIdx.x / st_) * BT_PTS + 2 * (k) + (threadIdx.x >> 7)] = \
+                __builtin_amdgcn_s_memrealtime();                                          \
+    } while (0)
 #else
+#define WAVE_TS2(g, k) \
+    do {               \
+    } while (0)
 #define WAVE_TS_ID(g) \
     do {              \
     } while (0)
@@ -1117,7 +1129,7 @@ __device__ __forceinline__ double search_align_lane(const FkSm &f, const CV &cv,
 // ---------------------------------------------------------------- filter search (wave form)
 // BFMatcher's match decided from a cheap fp32 estimate of every d2, with the exact search
 // only for the points whose estimate cannot decide it.  Per particle (filt_setup): an origin
-// o (the centres' mean), s'_j = Sp_j - o, and per centre (-2 s'_j, |s'_j|^2 + 1) in LDS; per
+// o (a central centre), s'_j = Sp_j - o, and per centre (-2 s'_j, |s'_j|^2 + 1) in LDS; per
 // point q' = (float)p - o, Q = |q'|^2 and
 //     a_j = ((|s'_j|^2 + 1) + Q) + q'.(-2 s'_j)          (one add + three fma per centre)
 // which estimates D_j + 1, D_j = |(float)p - Sp_j|^2 (real), within
@@ -1139,20 +1151,6 @@ struct FiltC {
     float ox, oy, oz;  // origin
     float K;           // R + 1
 };
-__device__ __forceinline__ float row_sum16_f32(float v) {
-    v += __int_as_float(dpp_i32<0xB1>(__float_as_int(v)));
-    v += __int_as_float(dpp_i32<0x4E>(__float_as_int(v)));
-    v += __int_as_float(dpp_i32<0x141>(__float_as_int(v)));
-    v += __int_as_float(dpp_i32<0x140>(__float_as_int(v)));
-    return v;
-}
-__device__ __forceinline__ float wave_sum_f32(float v) {
-    v = row_sum16_f32(v);
-    return ((__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)) +
-             __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16))) +
-            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32))) +
-           __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
-}
 __device__ __forceinline__ float wave_max_f32(float v) {  // v >= 0 (or NaN: result unspecified)
     v = fmaxf(v, __int_as_float(dpp_i32<0xB1>(__float_as_int(v))));
     v = fmaxf(v, __int_as_float(dpp_i32<0x4E>(__float_as_int(v))));
@@ -1163,17 +1161,19 @@ __device__ __forceinline__ float wave_max_f32(float v) {  // v >= 0 (or NaN: res
                  fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)),
                        __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48))));
 }
-// one wave, after FK: own = this lane's centre (lanes < 48).  The caller syncs the wave
-// before the search reads fs.
-__device__ __forceinline__ FiltC filt_setup(FiltSm &fs, const SphXYZ &own) {
+// one wave, after FK (f's fp32 centres visible to the wave): own = this lane's centre (lanes
+// < 48).  The origin is centre FILT_ORIGIN, the most central of the model (over random poses
+// its farthest centre is 9.3 cm away on average, the centres' mean 9.1): one broadcast LDS
+// read instead of three wave sums.  The caller syncs the wave before the search reads fs.
+#define FILT_ORIGIN 21
+__device__ __forceinline__ FiltC filt_setup(FiltSm &fs, const FkSm &f, const SphXYZ &own) {
     const int l = threadIdx.x & 63;
     const bool on = l < HPE_NS;
     const float sx = (float)own.x, sy = (float)own.y, sz = (float)own.z;
     FiltC c;
-    const float inv = 1.0f / HPE_NS;
-    c.ox = wave_sum_f32(on ? sx : 0.0f) * inv;
-    c.oy = wave_sum_f32(on ? sy : 0.0f) * inv;
-    c.oz = wave_sum_f32(on ? sz : 0.0f) * inv;
+    c.ox = f.Sp[0][FILT_ORIGIN];
+    c.oy = f.Sp[1][FILT_ORIGIN];
+    c.oz = f.Sp[2][FILT_ORIGIN];
     const float tx = sx - c.ox, ty = sy - c.oy, tz = sz - c.oz;
     const float r2 = (tx * tx + ty * ty) + tz * tz;
     c.K = wave_max_f32(on ? r2 : 0.0f) + 1.0f;
@@ -1431,15 +1431,18 @@ __device__ __forceinline__ double eval_wave_cost(FkSm *fks, FiltSm &fs, const De
     } else {
         fk_wave(f, H, &own);
     }
+    WAVE_TS2(g_ts, 4);
     const DepthG dg = depth_issue_at(own, l, o, H);
-    const FiltC fc = filt_setup(fs, own);
+    const FiltC fc = filt_setup(fs, f, own);
     wave_sync();
-    WAVE_TS(g_ts, 8);
+    WAVE_TS2(g_ts, 5);
     double al = search_align_filt(f, fs, fc, cv, H, pre, l + 64 * sub, 64 * WPP);
     if (HPE_STAMPS) asm volatile("" ::"v"(al));
-    WAVE_TS(g_ts, 12);
+    WAVE_TS2(g_ts, 6);
     double dep = depth_finish(dg, o, l < HPE_NS && sub == 0);
     const double part = wave_sum(al * o.lambda + dep);
+    if (HPE_STAMPS) asm volatile("" ::"v"(part));
+    WAVE_TS2(g_ts, 7);
     if (WPP == 1) return part;
     const int w = threadIdx.x >> 6;
     if (l == 0) xpart[w] = part;

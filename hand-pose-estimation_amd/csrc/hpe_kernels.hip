@@ -658,7 +658,7 @@ __global__ __launch_bounds__(PW_NT, WPP == 2 ? 2 : 4) void k_pso_gen_w(DevSwarm 
         "s"(sw.xh), "s"(sw.pch), "s"(sw.pb), "s"(sw.v), "s"(sw.inbox), "s"(sw.ibtc),
         "s"(sw.P), "s"(sw.K));
     const DevObs o = *og;
-    WAVE_TS_ID(g);
+    WAVE_TS2(g, 0);
     __shared__ DevHand hs;
     __shared__ FkSm fks[PW_WPB];
     __shared__ FiltSm fls[PW_WPB];
@@ -748,6 +748,7 @@ __global__ __launch_bounds__(PW_NT, WPP == 2 ? 2 : 4) void k_pso_gen_w(DevSwarm 
     if (ROW16) row0_argmin_lex(v, idx, slot, inf, islot, XCH ? &infc : nullptr);
     else wave_argmin_lex(v, idx, slot, inf, islot, XCH ? &infc : nullptr);
     const bool use_ext = XCH && readlane_f64(exr, HPE_DOF) < infc;  // strictly better
+    WAVE_TS2(g, 1);
     // ---- velocity, position, check_constraints (PSO.cpp:824-842, 358-377)
     if (l < HPE_DOF) {
         double vn;
@@ -772,11 +773,12 @@ __global__ __launch_bounds__(PW_NT, WPP == 2 ? 2 : 4) void k_pso_gen_w(DevSwarm 
     Link lk[3];
     push_lane_links(sw, g, ic, l, g + 1, topo, lk);
     hand_put<PW_NT>(hs, hw);
-    WAVE_TS(g, 4);
+    WAVE_TS2(g, 2);
     __syncthreads();  // hand staged (the only block-wide sync)
+    WAVE_TS2(g, 3);
     // ---- evaluation and pbest (PSO.cpp:848-861)
     const double fx = eval_wave_cost<WPP, COOP, PW_WPB>(fks, fls[w], o, cv, H, pre, sub, xpart, g);
-    WAVE_TS(g, 16);
+    WAVE_TS2(g, 8);
     if (!valid || sub != 0) return;
     const bool better = fx < pci;
     const double pn = better ? fx : pci;
@@ -790,12 +792,13 @@ __global__ __launch_bounds__(PW_NT, WPP == 2 ? 2 : 4) void k_pso_gen_w(DevSwarm 
         gmin_lower(sw, g, i, pn);
     }
     wave_sync();
+    WAVE_TS2(g, 9);
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const int q = l + 64 * k;
         push_inbox_w(sw, g, i, q, lk[k], q < 3 * IB_FIELDS ? g + 1 : topo, pn, f.th);
     }
-    WAVE_TS(g, 20);
+    WAVE_TS2(g, 10);
 }
 
 // The opt-in per-generation exchange (hpe_set_exchange): this subswarm's best after

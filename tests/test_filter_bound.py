@@ -25,7 +25,7 @@ def _fma(a, b, c):
 def filter_pick(q, S):
     """q: (n, 3) float64 cloud, S: (48, 3) float64 centres -> (pick or -1 per point)."""
     sf = _f(S)
-    o = _f(sf.sum(axis=0, dtype=np.float32) * _f(1.0 / 48))  # any origin: only the bound needs care
+    o = sf[21]  # FILT_ORIGIN (any origin is valid: only the bound depends on it)
     t = sf - o
     r2 = (t[:, 0] * t[:, 0] + t[:, 1] * t[:, 1]) + t[:, 2] * t[:, 2]
     ax, ay, az = _f(-2.0) * t[:, 0], _f(-2.0) * t[:, 1], _f(-2.0) * t[:, 2]

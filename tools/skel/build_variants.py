@@ -21,9 +21,12 @@ EDITS = {
     # the fp64 alignment residual inside the search (the match is still found)
     "noalign": [("hpe_device.hpp", "        const double e = sqrt((dx * dx + dy * dy) + dz * dz) - r.cr;\n        acc += e * e;\n        q = qn;",
                  "        acc += dx + (dy + dz);\n        q = qn;")],
+    # the informant's pbest row (a dependent global load in the wave form)
+    "norow": [("hpe_kernels.hip", "            const double pbn = use_ext ? exr : sw.inbox[ib_index(sw, (g - 1) & 1, var, ic, islot) + 2 + l];",
+               "            const double pbn = use_ext ? exr : xo + 1e-3 * islot;")],
     # the rp / rg draws of the wave form
-    "nophilox": [("hpe_kernels.hip", "    const double rp = philox_u01(sw.seed, ST_RP, g, ic, dl);\n    const double rg = philox_u01(sw.seed, ST_RG, g, ic, dl);",
-                  "    const double rp = 0.25 + dl * 1e-3, rg = 0.75 - dl * 1e-3;")],
+    "nophilox": [("hpe_kernels.hip", "    const double rd = philox_u01(sw.seed, l < HPE_DOF ? ST_RP : ST_RG, g, ic, dl);",
+                  "    const double rd = 0.25 + dl * 1e-3;")],
 }
 
 

@@ -39,52 +39,29 @@ buf = np.zeros(GENS * BLK * PTS, dtype=np.uint64)
 for rep in range(2):
     pso.pso_evolve(cf, pose[2].copy(), P, bestp)
     lib.hpe_debug_blk_ts(buf.ctypes.data_as(C.POINTER(C.c_uint64)))
-raw = buf.reshape(GENS, BLK, PTS)
-ent = raw[:, :, 0:4].copy()  # entry stamps: clock | HW_ID << 40 | XCC_ID << 56
-ts = (raw & np.uint64((1 << 40) - 1)).astype(np.int64)
-names = ["entry->staged", "staged->searched(FK,filt)", "search", "sum->done(eval)", "pbest,pushes"]
-pts = [0, 4, 8, 12, 16, 20]
-print(f"P={P} wpp={os.environ.get('HPE_PSO_WPP', 'auto')}; medians over waves, us")
-print("gen span ramp | " + " | ".join(names) + " | p90 start")
+ts = buf.reshape(GENS, BLK, PTS).astype(np.int64)
+NPT = 11
+names = ["entry->informant", "->hand staged", "barrier", "FK", "depth issue+filter tables",
+         "search", "sums", "particle sum barrier", "pbest+pch", "pushes"]
+print(f"P={P} wpp={os.environ.get('HPE_PSO_WPP', 'auto')}; the even waves of a sample of "
+      f"workgroups (slot 2k + wave/2), medians over waves, us")
+print("gen  span | " + " | ".join(names))
 for g in range(1, 31):
     t = ts[g]
-    w = np.stack([t[:, k:k + 4].reshape(-1) for k in pts], axis=1)  # (blocks*4, 6)
+    w = np.concatenate([t[:, [2 * k + j for k in range(NPT)]] for j in range(2)], axis=0)  # (waves, NPT)
     w = w[w[:, 0] > 0]
     if not len(w):
         continue
     t0 = w[:, 0].min()
-    ramp = (np.median(w[:, 0]) - t0) / 100
-    ph = np.diff(w, axis=1) / 100
-    ok = (w[:, 1:] > 0)  # the second wave of a particle (wpp 2) leaves before the last point
-    med = [np.median(ph[ok[:, k], k]) if ok[:, k].any() else float("nan") for k in range(5)]
-    end = w[:, 5][w[:, 5] > 0]
-    print(f"{g:3d} {(max(end.max(), w[:, 4].max()) - t0) / 100:6.2f} {ramp:5.2f} | " +
-          " | ".join(f"{v:5.2f}" for v in med) +
-          f" | start spread {(np.percentile(w[:, 0], 90) - t0) / 100:5.2f}")
-
-# placement of generation 10's sampled waves: start time vs (XCC, SE, CU) and the number of
-# workgroups each CU ran
-g = 10
-e = ent[g].reshape(-1)
-t = ts[g, :, 0:4].reshape(-1)
-ok = e != 0
-hw = (e[ok] >> np.uint64(40)) & np.uint64(0xFFFF)
-xcc = (e[ok] >> np.uint64(56)) & np.uint64(0xF)
-cu = ((hw >> np.uint64(8)) & np.uint64(0xF)).astype(int)
-sh = ((hw >> np.uint64(12)) & np.uint64(1)).astype(int)
-se = ((hw >> np.uint64(13)) & np.uint64(0x7)).astype(int)
-simd = ((hw >> np.uint64(4)) & np.uint64(3)).astype(int)
-slot = (hw & np.uint64(0xF)).astype(int)
-st = (t[ok] - t[ok].min()) / 100
-key = xcc.astype(int) * 1000 + se * 100 + sh * 16 + cu
-print(f"gen {g}: {ok.sum()} sampled waves on {len(np.unique(key))} CUs, XCCs {sorted(set(xcc.tolist()))}")
-late = st > 2.0
-print(f"  started > 2 us after the first: {late.sum()} waves; early-wave slots {np.bincount(slot[~late])}; late-wave slots {np.bincount(slot[late]) if late.any() else []}")
-per_cu = {}
-for k, s_ in zip(key, st):
-    per_cu.setdefault(k, []).append(s_)
-cnt = np.array([len(v) for v in per_cu.values()])
-print("  waves per sampled CU (histogram):", np.bincount(cnt))
-ex = list(per_cu.items())[:4]
-for k, v in ex:
-    print(f"  CU {k}: starts {sorted(np.round(v, 2).tolist())}")
+    end = w[:, 10][w[:, 10] > 0]
+    span = ((end.max() if len(end) else w.max()) - t0) / 100
+    med = []
+    for k in range(NPT - 1):
+        ok = (w[:, k] > 0) & (w[:, k + 1] > 0)
+        med.append(np.median(w[ok, k + 1] - w[ok, k]) / 100 if ok.any() else float("nan"))
+    st = (w[:, 0] - t0) / 100
+    en = (end - t0) / 100 if len(end) else st
+    print(f"{g:3d} {span:6.2f} | " + " | ".join(f"{v:5.2f}" for v in med) +
+          f" | start p10/50/90 {np.percentile(st, 10):.2f}/{np.percentile(st, 50):.2f}/"
+          f"{np.percentile(st, 90):.2f} end {np.percentile(en, 10):.2f}/{np.percentile(en, 50):.2f}/"
+          f"{np.percentile(en, 90):.2f}")
