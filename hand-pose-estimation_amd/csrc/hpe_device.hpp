@@ -153,6 +153,15 @@ struct __align__(16) FkSm {
     double sn[24], cs[24];   // 3 global + 20 digit angles
 };
 
+// The filter search's per-particle tables (bf_filter_lane).
+struct __align__(16) FiltSm {
+    float ax[HPE_NS], ay[HPE_NS], az[HPE_NS], aw[HPE_NS];  // -2 s'_j, |s'_j|^2 + 1
+};
+struct FiltC {
+    float ox, oy, oz;  // origin
+    float K;           // R + 1
+};
+
 // Block-level workspace (one particle per workgroup).
 struct __align__(16) Smem {
     DevHand hand;  // hand constants staged from HBM (lane-indexed reads stay in LDS)
@@ -162,6 +171,8 @@ struct __align__(16) Smem {
     int iscal[16];
     double draws[2 * HPE_DOF];  // rp, rg of the generation (k_pso_gen)
     double pbr[32];             // own pbest row at entry (k_pso_gen's pushes)
+    FiltSm flt;                 // the filter search's tables (cal_cost of large clouds)
+    FiltC fltc;
 };
 
 // Global-memory pointers.  Pointers read from memory (the frame descriptor DevObs) are
@@ -1144,13 +1155,6 @@ __device__ __forceinline__ double search_align_lane(const FkSm &f, const CV &cv,
 // <= 8 u): j* is BFMatcher's match, whatever the ties in the estimate.  Otherwise (two centres
 // within the bound: ~0.06 % of points on the bench sequence), bf_search_lane decides exactly.
 // NaN or infinite inputs fail the test (comparisons with NaN are false) and go the exact way.
-struct __align__(16) FiltSm {
-    float ax[HPE_NS], ay[HPE_NS], az[HPE_NS], aw[HPE_NS];  // -2 s'_j, |s'_j|^2 + 1
-};
-struct FiltC {
-    float ox, oy, oz;  // origin
-    float K;           // R + 1
-};
 __device__ __forceinline__ float wave_max_f32(float v) {  // v >= 0 (or NaN: result unspecified)
     v = fmaxf(v, __int_as_float(dpp_i32<0xB1>(__float_as_int(v))));
     v = fmaxf(v, __int_as_float(dpp_i32<0x4E>(__float_as_int(v))));
@@ -1161,15 +1165,15 @@ __device__ __forceinline__ float wave_max_f32(float v) {  // v >= 0 (or NaN: res
                  fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)),
                        __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48))));
 }
-// one wave, after FK (f's fp32 centres visible to the wave): own = this lane's centre (lanes
-// < 48).  The origin is centre FILT_ORIGIN, the most central of the model (over random poses
-// its farthest centre is 9.3 cm away on average, the centres' mean 9.1): one broadcast LDS
-// read instead of three wave sums.  The caller syncs the wave before the search reads fs.
+// One wave, after FK (f's fp32 centres visible to the wave): (sx, sy, sz) = this lane's fp32
+// centre, on = lane < 48.  The origin is centre FILT_ORIGIN, the most central of the model
+// (over random poses its farthest centre is 9.3 cm away on average, the centres' mean 9.1):
+// one broadcast LDS read instead of three wave sums.  The caller syncs before the search
+// reads fs.
 #define FILT_ORIGIN 21
-__device__ __forceinline__ FiltC filt_setup(FiltSm &fs, const FkSm &f, const SphXYZ &own) {
+__device__ __forceinline__ FiltC filt_setup_f(FiltSm &fs, const FkSm &f, float sx, float sy,
+                                              float sz, bool on) {
     const int l = threadIdx.x & 63;
-    const bool on = l < HPE_NS;
-    const float sx = (float)own.x, sy = (float)own.y, sz = (float)own.z;
     FiltC c;
     c.ox = f.Sp[0][FILT_ORIGIN];
     c.oy = f.Sp[1][FILT_ORIGIN];
@@ -1184,6 +1188,11 @@ __device__ __forceinline__ FiltC filt_setup(FiltSm &fs, const FkSm &f, const Sph
         fs.aw[l] = r2 + 1.0f;
     }
     return c;
+}
+// the same from this lane's fp64 centre in registers (FK's own)
+__device__ __forceinline__ FiltC filt_setup(FiltSm &fs, const FkSm &f, const SphXYZ &own) {
+    const bool on = (threadIdx.x & 63) < HPE_NS;
+    return filt_setup_f(fs, f, (float)own.x, (float)own.y, (float)own.z, on);
 }
 __device__ __forceinline__ unsigned med3_u32(unsigned a, unsigned b, unsigned c) {
     unsigned r;
@@ -1463,7 +1472,7 @@ __device__ __forceinline__ CloudGlobal obs_cloud(const DevObs &o) {
 // FK = false: the caller has already placed the centres in sm.fk.S / Sp (hpe_eval_spheres).
 // own_w0 (FK = false): the centres wave 0's FK (run by the caller) left in its registers,
 // projected here without re-reading them from LDS; otherwise read from sm.fk.
-template <int MODE, int NT, bool FK = true, class CV>
+template <int MODE, int NT, bool FK = true, bool FILT = false, class CV>
 __device__ __forceinline__ double eval_block(Smem &sm, const DevObs &o, const CV &cv,
                                              const DevHand *__restrict__ H,
                                              int32_t *__restrict__ match, Pt pre,
@@ -1480,6 +1489,24 @@ __device__ __forceinline__ double eval_block(Smem &sm, const DevObs &o, const CV
         own = *own_w0;
     }
     sc.lap(10);
+    // FILT (the host's choice for frames of more than NT / 2 points, N = full): cal_cost over
+    // the HBM cloud by the filter search, one thread per point (bf_filter_lane: the same
+    // matches, about half the instructions of the lane-pair search); wave 0 builds the
+    // tables, one barrier publishes them.  Every kernel of a frame makes the same choice.
+    constexpr bool filt = FILT && MODE == EV_COST && std::is_same<CV, CloudGlobal>::value;
+    Pt pre1{0.0, 0.0, 0.0};
+    FiltC fc{0.f, 0.f, 0.f, 0.f};
+    if constexpr (filt) {
+        pre1 = load_pt1(cv, t);
+        if (t < 64) {
+            const int sl = t < HPE_NS ? t : 0;
+            const FiltC c = filt_setup_f(sm.flt, sm.fk, sm.fk.Sp[0][sl], sm.fk.Sp[1][sl],
+                                         sm.fk.Sp[2][sl], t < HPE_NS);
+            if (t == 0) sm.fltc = c;
+        }
+        __syncthreads();
+        fc = sm.fltc;
+    }
     // wave 0 issues the depth gathers first (after the barrier: the other waves start
     // searching at once): their latency hides under the search
     DepthG dg{0.0, 0.0, 0.0, 0.f, false};
@@ -1493,6 +1520,7 @@ __device__ __forceinline__ double eval_block(Smem &sm, const DevObs &o, const CV
     if (MODE == EV_COST2_FROZEN) al = align_frozen(sm.fk, cv, H, match, t, NT);
     else if (MODE == EV_COST2_CORR || MODE == EV_COST_STORE)
         al = search_align<NT, true>(sm.fk, cv, H, match, pre);
+    else if (filt) al = search_align_filt(sm.fk, sm.flt, fc, cv, H, pre1, t, NT);
     else al = search_align<NT, false>(sm.fk, cv, H, nullptr, pre, -1, g_ts);
     if (young) __builtin_amdgcn_s_setprio(0);
     const bool coll = (MODE == EV_COST2_CORR || MODE == EV_COST2_FROZEN);

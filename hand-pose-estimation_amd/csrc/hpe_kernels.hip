@@ -250,7 +250,7 @@ __device__ __forceinline__ bool split_arrive(const DevSwarm &sw, int g, int i, i
 // generate_particles + the initial evaluation (PSO.cpp:56-74, 748-763).  SPLIT > 1: the
 // split form of k_pso_gen_split (the same slices and sums, so a particle's cost of the same
 // theta is the same bits in both kernels).
-template <int NT, int SPLIT>
+template <int NT, int SPLIT, bool FILT = false>
 __device__ __forceinline__ void pso_init_body(const DevSwarm &sw, const double *__restrict__ x0,
                                               const DevObs *__restrict__ og,
                                               const DevHand *__restrict__ Hg) {
@@ -284,7 +284,7 @@ __device__ __forceinline__ void pso_init_body(const DevSwarm &sw, const double *
     if (sw.ext && i == 0 && slice == 0 && t == 0) sw.ext[HPE_DOF] = __builtin_inf();  // no candidate yet
     hand_put<NT>(sm.hand, hw);
     __syncthreads();
-    double c = eval_block<EV_COST, NT>(sm, o, cv, H, nullptr, pre, BT_GENS, nullptr, slice == 0);
+    double c = eval_block<EV_COST, NT, true, FILT>(sm, o, cv, H, nullptr, pre, BT_GENS, nullptr, slice == 0);
     if constexpr (SPLIT > 1) {
         if (!split_arrive<SPLIT>(sw, 0, i, slice, c, sm)) return;
     }
@@ -295,9 +295,10 @@ __device__ __forceinline__ void pso_init_body(const DevSwarm &sw, const double *
     push_inbox(sw, 0, i, q, lk, 1, c, sm.fk.th);
 }
 
+template <bool FILT>
 __global__ __launch_bounds__(HPE_NT) void k_pso_init(DevSwarm sw, const double *__restrict__ x0,
                                                      const DevObs *__restrict__ og, const DevHand *__restrict__ Hg) {
-    pso_init_body<HPE_NT, 1>(sw, x0, og, Hg);
+    pso_init_body<HPE_NT, 1, FILT>(sw, x0, og, Hg);
 }
 
 // One fused generation g >= 1 (PSO.cpp:781-879).  Wave 0 carries the serial part: every
@@ -317,7 +318,7 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_init(DevSwarm sw, const double *
 // slots (sw.K <= 15, the host's choice of instantiation): the informant argmin runs on one
 // 16-lane DPP row.  (A run-time K test left one body for both cases: the compiler no longer
 // duplicated the kernel per case, and the generation ran 0.15 us slower.)
-template <int NT, int SPLIT, bool XCH = false, bool ROW16 = true>
+template <int NT, int SPLIT, bool XCH = false, bool ROW16 = true, bool FILT = false>
 __device__ __forceinline__ void pso_gen_body(const DevSwarm &sw, const DevObs *__restrict__ og,
                                              const DevHand *__restrict__ Hg, int g, double W1,
                                              double C1, double C2, const InboxCounts &kin) {
@@ -504,7 +505,7 @@ __device__ __forceinline__ void pso_gen_body(const DevSwarm &sw, const DevObs *_
     const double pci = sm.dscal[4];
     const Link lk0 = load_link(sw, g, i, q, topo, q >= 3 * IB_FIELDS);
     // ---- evaluation and pbest (PSO.cpp:848-861)
-    double fx = eval_block<EV_COST, NT, false>(sm, o, cv, H, nullptr, pre, g, &own0, slice == 0);
+    double fx = eval_block<EV_COST, NT, false, FILT>(sm, o, cv, H, nullptr, pre, g, &own0, slice == 0);
     BLK_TS(g, 4);
     if constexpr (SPLIT > 1) {
         if (!split_arrive<SPLIT>(sw, g, i, slice, fx, sm)) return;
@@ -527,19 +528,19 @@ __device__ __forceinline__ void pso_gen_body(const DevSwarm &sw, const DevObs *_
     sc.span(5);
 }
 
-template <bool ROW16>
+template <bool ROW16, bool FILT>
 __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *__restrict__ og,
                                                     const DevHand *__restrict__ Hg, int g,
                                                     double W1, double C1, double C2,
                                                     InboxCounts kin) {
-    pso_gen_body<HPE_NT, 1, false, ROW16>(sw, og, Hg, g, W1, C1, C2, kin);
+    pso_gen_body<HPE_NT, 1, false, ROW16, FILT>(sw, og, Hg, g, W1, C1, C2, kin);
 }
-template <bool ROW16>
+template <bool ROW16, bool FILT>
 __global__ __launch_bounds__(HPE_NT) void k_pso_gen_x(DevSwarm sw, const DevObs *__restrict__ og,
                                                       const DevHand *__restrict__ Hg, int g,
                                                       double W1, double C1, double C2,
                                                       InboxCounts kin) {
-    pso_gen_body<HPE_NT, 1, true, ROW16>(sw, og, Hg, g, W1, C1, C2, kin);
+    pso_gen_body<HPE_NT, 1, true, ROW16, FILT>(sw, og, Hg, g, W1, C1, C2, kin);
 }
 
 // Large clouds (N > RF_STAGE_MAX, e.g. the full ~9.3k-point cloud): SPLIT workgroups of 256
@@ -888,7 +889,7 @@ __device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v,
 // eval_block on the same theta: the gbest cost is kept, bit for bit (same_eval: the
 // generations used the workgroup form).  Otherwise (nothing beat 1e100, bestp = zeros)
 // the block evaluates it.
-template <bool TAIL = false>
+template <bool TAIL = false, bool FILT = false>
 __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__restrict__ out,
                                                       const DevObs *og = nullptr,
                                                       const DevHand *__restrict__ Hg = nullptr,
@@ -1099,7 +1100,7 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
         const CloudGlobal cv = obs_cloud(o);
         const Pt pre = load_pt(cv, t);
         __syncthreads();
-        const double c = eval_block<EV_COST, HPE_NT>(sm, o, cv, &sm.hand, nullptr, pre);
+        const double c = eval_block<EV_COST, HPE_NT, true, FILT>(sm, o, cv, &sm.hand, nullptr, pre);
         if (t == 0) {
             out[HPE_DOF] = c;
             if (hist) hist[HPE_DOF] = c;
