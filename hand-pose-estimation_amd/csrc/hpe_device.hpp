@@ -153,7 +153,11 @@ struct __align__(16) FkSm {
     double sn[24], cs[24];   // 3 global + 20 digit angles
 };
 
-// The filter search's per-particle tables (bf_filter_lane).
+// The filter search's per-particle tables (bf_filter_lane).  FILT_PTS: points per pass in
+// the workgroup form's filter search (one table read serves them all).
+#ifndef FILT_PTS
+#define FILT_PTS 2
+#endif
 struct __align__(16) FiltSm {
     float ax[HPE_NS], ay[HPE_NS], az[HPE_NS], aw[HPE_NS];  // -2 s'_j, |s'_j|^2 + 1
 };
@@ -1266,6 +1270,127 @@ __device__ __forceinline__ BfOut bf_filter_lane(const FkSm &f, const FiltSm &fs,
     }
     return bf_search_lane(f, H, qx, qy, qz);
 }
+// Two points per pass sharing every table read (the workgroup form at N = full, where a
+// thread has many points and registers to spare): filt_half for points 0 and 1.
+template <int J0, int U>
+__device__ __forceinline__ void filt_half2(const FiltSm &fs, const float (&px)[U],
+                                           const float (&py)[U], const float (&pz)[U],
+                                           const float (&Q)[U], Min2 (&out)[U]) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    unsigned key[U][24];
+#pragma unroll
+    for (int j = 0; j < 24; j += 4) {
+        const f4 ax = *(const f4 *)(fs.ax + J0 + j), ay = *(const f4 *)(fs.ay + J0 + j),
+                 az = *(const f4 *)(fs.az + J0 + j), aw = *(const f4 *)(fs.aw + J0 + j);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const f2 wx = h ? f2{ax.z, ax.w} : f2{ax.x, ax.y};
+            const f2 wy = h ? f2{ay.z, ay.w} : f2{ay.x, ay.y};
+            const f2 wz = h ? f2{az.z, az.w} : f2{az.x, az.y};
+            const f2 ww = h ? f2{aw.z, aw.w} : f2{aw.x, aw.y};
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                f2 a = ww + f2{Q[u], Q[u]};
+                a = __builtin_elementwise_fma(f2{px[u], px[u]}, wx, a);
+                a = __builtin_elementwise_fma(f2{py[u], py[u]}, wy, a);
+                a = __builtin_elementwise_fma(f2{pz[u], pz[u]}, wz, a);
+                key[u][j + 2 * h] = __float_as_uint(a.x);
+                key[u][j + 2 * h + 1] = __float_as_uint(a.y);
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#define HPE_FKEY(J) asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(key[u][J]) : "v"(key[u][J]), "s"(0xFFFFFFC0u), "i"(J0 + J));
+        HPE_FKEY(0) HPE_FKEY(1) HPE_FKEY(2) HPE_FKEY(3) HPE_FKEY(4) HPE_FKEY(5) HPE_FKEY(6)
+        HPE_FKEY(7) HPE_FKEY(8) HPE_FKEY(9) HPE_FKEY(10) HPE_FKEY(11) HPE_FKEY(12) HPE_FKEY(13)
+        HPE_FKEY(14) HPE_FKEY(15) HPE_FKEY(16) HPE_FKEY(17) HPE_FKEY(18) HPE_FKEY(19) HPE_FKEY(20)
+        HPE_FKEY(21) HPE_FKEY(22) HPE_FKEY(23)
+#undef HPE_FKEY
+        Min2 L[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) L[k] = min2_leaf(key[u][3 * k], key[u][3 * k + 1], key[u][3 * k + 2]);
+        out[u] = min2_merge3(min2_merge3(L[0], L[1], L[2]), min2_merge3(L[3], L[4], L[5]),
+                             min2_merge2(L[6], L[7]));
+    }
+}
+// bf_filter_lane for U points (the same test per point, the exact search where it fails)
+template <int U>
+__device__ __forceinline__ void bf_filter_lane2(const FkSm &f, const FiltSm &fs, const FiltC &c,
+                                                const DevHand *__restrict__ H, const float (&qx)[U],
+                                                const float (&qy)[U], const float (&qz)[U],
+                                                BfOut (&r)[U]) {
+    float px[U], py[U], pz[U], Q[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        px[u] = qx[u] - c.ox;
+        py[u] = qy[u] - c.oy;
+        pz[u] = qz[u] - c.oz;
+        Q[u] = (px[u] * px[u] + py[u] * py[u]) + pz[u] * pz[u];
+    }
+    Min2 ma[U], mb[U];
+    filt_half2<0, U>(fs, px, py, pz, Q, ma);
+    filt_half2<24, U>(fs, px, py, pz, Q, mb);
+    constexpr float U64 = 64.0f / 16777216.0f, U32 = 32.0f / 16777216.0f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const Min2 m = min2_merge2(ma[u], mb[u]);
+        const float E = (Q[u] + c.K) * U64;
+        const float v1 = __uint_as_float(m.m | 63u), v2 = __uint_as_float(m.s & ~63u);
+        const float M = (v1 + E) * U32;
+        if ((v2 - v1 > E * 2.0f + M) && (E < 0.5f)) {
+            const int ic = (int)(m.m & 63u);
+            r[u] = BfOut{ic, ic, f.S[ic][0], f.S[ic][1], f.S[ic][2], H->radii[ic]};
+        } else {
+            r[u] = bf_search_lane(f, H, qx[u], qy[u], qz[u]);
+        }
+    }
+}
+// search_align_filt over points p0, p0 + step, ... U per pass (p, p + step, ...), the next
+// pass's points loaded one pass ahead; pre = the point p0.  A pass's points past the cloud
+// are evaluated at a clamped index and not added.
+template <int U, class CV>
+__device__ __forceinline__ double search_align_filt2(const FkSm &f, const FiltSm &fs,
+                                                     const FiltC &c, const CV &cv,
+                                                     const DevHand *__restrict__ H, Pt pre,
+                                                     int p0, int step) {
+    double acc = 0.0;
+    const int n1 = cv.n - 1;
+    Pt q[U];
+    q[0] = pre;
+#pragma unroll
+    for (int u = 1; u < U; ++u) {
+        const int pu = min(p0 + u * step, n1);
+        q[u] = Pt{cv.cx[pu], cv.cy[pu], cv.cz[pu]};
+    }
+    for (int p = p0; p < cv.n; p += U * step) {
+        asm volatile("" ::: "memory");  // the tables re-read from LDS per pass (registers)
+        Pt qn[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int pu = min(p + (U + u) * step, n1);
+            qn[u] = Pt{cv.cx[pu], cv.cy[pu], cv.cz[pu]};
+        }
+        float qx[U], qy[U], qz[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            qx[u] = (float)q[u].x;
+            qy[u] = (float)q[u].y;
+            qz[u] = (float)q[u].z;
+        }
+        BfOut r[U];
+        bf_filter_lane2<U>(f, fs, c, H, qx, qy, qz, r);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const double dx = q[u].x - r[u].cx, dy = q[u].y - r[u].cy, dz = q[u].z - r[u].cz;
+            const double e = sqrt((dx * dx + dy * dy) + dz * dz) - r[u].cr;
+            if (u == 0 || p + u * step < cv.n) acc += e * e;
+            q[u] = qn[u];
+        }
+    }
+    return acc;
+}
 // points p0, p0 + step, ... of an HBM cloud, the next one loaded one ahead; pre = that of p0
 template <class CV>
 __device__ __forceinline__ double search_align_filt(const FkSm &f, const FiltSm &fs,
@@ -1520,7 +1645,7 @@ __device__ __forceinline__ double eval_block(Smem &sm, const DevObs &o, const CV
     if (MODE == EV_COST2_FROZEN) al = align_frozen(sm.fk, cv, H, match, t, NT);
     else if (MODE == EV_COST2_CORR || MODE == EV_COST_STORE)
         al = search_align<NT, true>(sm.fk, cv, H, match, pre);
-    else if (filt) al = search_align_filt(sm.fk, sm.flt, fc, cv, H, pre1, t, NT);
+    else if (filt) al = search_align_filt2<FILT_PTS>(sm.fk, sm.flt, fc, cv, H, pre1, t, NT);
     else al = search_align<NT, false>(sm.fk, cv, H, nullptr, pre, -1, g_ts);
     if (young) __builtin_amdgcn_s_setprio(0);
     const bool coll = (MODE == EV_COST2_CORR || MODE == EV_COST2_FROZEN);
