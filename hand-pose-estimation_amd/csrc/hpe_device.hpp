@@ -1570,7 +1570,10 @@ __device__ __forceinline__ double eval_wave_cost(FkSm *fks, FiltSm &fs, const De
     const FiltC fc = filt_setup(fs, f, own);
     wave_sync();
     WAVE_TS2(g_ts, 5);
-    double al = search_align_filt(f, fs, fc, cv, H, pre, l + 64 * sub, 64 * WPP);
+    // two or four waves per particle (small swarms, registers to spare): two points per
+    // pass share each table read; one wave per particle stays at 128 VGPRs with one
+    double al = WPP > 1 ? search_align_filt2<2>(f, fs, fc, cv, H, pre, l + 64 * sub, 64 * WPP)
+                        : search_align_filt(f, fs, fc, cv, H, pre, l + 64 * sub, 64 * WPP);
     if (HPE_STAMPS) asm volatile("" ::"v"(al));
     WAVE_TS2(g_ts, 6);
     double dep = depth_finish(dg, o, l < HPE_NS && sub == 0);
