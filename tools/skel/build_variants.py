@@ -24,6 +24,12 @@ EDITS = {
     # the informant's pbest row (a dependent global load in the wave form)
     "norow": [("hpe_kernels.hip", "            const double pbn = use_ext ? exr : sw.inbox[ib_index(sw, (g - 1) & 1, var, ic, islot) + 2 + l];",
                "            const double pbn = use_ext ? exr : xo + 1e-3 * islot;")],
+    # the workgroup form's depth term (wave 0's projection, gathers and finish)
+    "blknodepth": [("hpe_device.hpp", "    if (t < 64 && with_depth) dg = (FK || own_w0) ? depth_issue_at(own, t, o, H) : depth_issue(sm.fk, t, o, H);",
+                    "    if (false) dg = depth_issue(sm.fk, t, o, H);")],
+    # the workgroup form's correspondence search (cal_cost at N <= 256)
+    "blknosearch": [("hpe_device.hpp", "    else al = search_align<NT, false>(sm.fk, cv, H, nullptr, pre, -1, g_ts);",
+                     "    else al = 0.0;")],
     # the rp / rg draws of the wave form
     "nophilox": [("hpe_kernels.hip", "    const double rd = philox_u01(sw.seed, l < HPE_DOF ? ST_RP : ST_RG, g, ic, dl);",
                   "    const double rd = 0.25 + dl * 1e-3;")],
