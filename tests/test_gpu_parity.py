@@ -468,17 +468,22 @@ def test_wave_form_cooperative_fk_bit_identical(oracle, ora_hand, np_hand, wpp, 
     assert abs(out["1"][1] - rc) <= 1e-8 * abs(rc)
 
 
+@pytest.mark.parametrize("form", ["wave", "wave2", "block"])
 @pytest.mark.parametrize("n_ties", [400, 4000])
-def test_wave_form_filter_search_ties(oracle, ora_hand, n_ties, monkeypatch):
-    """The wave form's filter search (hpe_device.hpp bf_filter_lane) on points that defeat
+def test_wave_form_filter_search_ties(oracle, ora_hand, n_ties, form, monkeypatch):
+    """The filter search (hpe_device.hpp bf_filter_lane: the wave form at one and two waves
+    per particle, and the workgroup form's cal_cost above 256 points) on points that defeat
     its estimate: float midpoints of centre pairs (exact and near ties, decided by the exact
-    search) and the centres themselves (d2 = 0), with a swarm whose particles all sit at the
-    pose the cloud was built from (std 0): every evaluation of both wave-form kernels (init and
-    one generation) must equal the oracle's cal_cost, whose match takes the first of equal
-    distances.  A wrong pick changes the alignment term (the radii differ)."""
+    search), the centres themselves (d2 = 0) and far outliers (the error bound E >= 0.5 sends
+    them the exact way), with a swarm whose particles all sit at the pose the cloud was built
+    from (std 0): every evaluation of the init and generation kernels must equal the oracle's
+    cal_cost, whose match takes the first of equal distances.  A wrong pick changes the
+    alignment term (the radii differ)."""
     import hpe
     import oracle_c
-    monkeypatch.setenv("HPE_PSO_FORM", "wave")
+    monkeypatch.setenv("HPE_PSO_FORM", "block" if form == "block" else "wave")
+    if form != "block":
+        monkeypatch.setenv("HPE_PSO_WPP", "2" if form == "wave2" else "1")
     gh = hpe.reference_hand(device=0)
     th = oracle_np.X0
     S = oracle.build(ora_hand, th).astype(np.float32).astype(np.float64)
@@ -488,6 +493,10 @@ def test_wave_form_filter_search_ties(oracle, ora_hand, n_ties, monkeypatch):
         a, b = rng.choice(48, 2, replace=False)
         pts.append(0.5 * (S[a] + S[b]))
     pts += list(S)
+    for k in range(6):  # outliers 400 and 1200 cm from the hand (E >= 0.5 from ~360 cm on)
+        v = np.zeros(3)
+        v[k % 3] = (-1) ** k * (400.0 if k < 3 else 1200.0)
+        pts.append(S[21] + v)
     cloud = np.array(pts)
     depth = np.zeros((240, 320)); dt = np.zeros((240, 320), np.float32)
     K = np.array([[241.42, 0, 160], [0, 241.42, 120], [0, 0, 1.0]])

@@ -30,6 +30,12 @@ EDITS = {
     # the workgroup form's correspondence search (cal_cost at N <= 256)
     "blknosearch": [("hpe_device.hpp", "    else al = search_align<NT, false>(sm.fk, cv, H, nullptr, pre, -1, g_ts);",
                      "    else al = 0.0;")],
+    # mutation check of the filter tie test: the filter's estimate accepted without its bound
+    # (no exact fallback; results wrong on near ties)
+    "nofallback": [("hpe_device.hpp", "        if ((v2 - v1 > E * 2.0f + M) && (E < 0.5f)) {\n            const int ic = (int)(m.m & 63u);",
+                    "        if (true) {\n            const int ic = (int)(m.m & 63u);"),
+                   ("hpe_device.hpp", "    if ((v2 - v1 > E * 2.0f + M) && (E < 0.5f)) {\n        const int ic = (int)(r.m & 63u);",
+                    "    if (true) {\n        const int ic = (int)(r.m & 63u);")],
     # the rp / rg draws of the wave form
     "nophilox": [("hpe_kernels.hip", "    const double rd = philox_u01(sw.seed, l < HPE_DOF ? ST_RP : ST_RG, g, ic, dl);",
                   "    const double rd = 0.25 + dl * 1e-3;")],
