@@ -36,6 +36,9 @@ EDITS = {
                     "        if (true) {\n            const int ic = (int)(m.m & 63u);"),
                    ("hpe_device.hpp", "    if ((v2 - v1 > E * 2.0f + M) && (E < 0.5f)) {\n        const int ic = (int)(r.m & 63u);",
                     "    if (true) {\n        const int ic = (int)(r.m & 63u);")],
+    # the wave form with eight waves per workgroup (same residency: two workgroups per CU)
+    "wpb8": [("hpe_kernels.hip", "#define PW_WPB 4", "#define PW_WPB 8"),
+             ("hpe_kernels.hip", "__launch_bounds__(PW_NT, WPP == 2 ? 2 : 4)", "__launch_bounds__(PW_NT, WPP == 2 ? 1 : 2)")],
     # the rp / rg draws of the wave form
     "nophilox": [("hpe_kernels.hip", "    const double rd = philox_u01(sw.seed, l < HPE_DOF ? ST_RP : ST_RG, g, ic, dl);",
                   "    const double rd = 0.25 + dl * 1e-3;")],
