@@ -39,6 +39,17 @@ EDITS = {
     # the wave form with eight waves per workgroup (same residency: two workgroups per CU)
     "wpb8": [("hpe_kernels.hip", "#define PW_WPB 4", "#define PW_WPB 8"),
              ("hpe_kernels.hip", "__launch_bounds__(PW_NT, WPP == 2 ? 2 : 4)", "__launch_bounds__(PW_NT, WPP == 2 ? 1 : 2)")],
+    # every depth / DT gather at pixel 0 (the gathers' latency and traffic)
+    "nogather": [("hpe_device.hpp", "    const int pix = d.in ? (int)dy * HPE_IMG_W + (int)dx : 0;\n",
+                  "    const int pix = 0;\n")],
+    # the workgroup form's inbox payload rows (waves 1..7's round-1 loads)
+    "blknorow": [("hpe_kernels.hip", "            a[k] = src[vr * var_stride + off];",
+                  "            a[k] = (double)(vr + off);")],
+    # both (the rows' own traffic, with the gathers' taken out)
+    "blknorow_nogather": [("hpe_kernels.hip", "            a[k] = src[vr * var_stride + off];",
+                           "            a[k] = (double)(vr + off);"),
+                          ("hpe_device.hpp", "    const int pix = d.in ? (int)dy * HPE_IMG_W + (int)dx : 0;\n",
+                           "    const int pix = 0;\n")],
     # the rp / rg draws of the wave form
     "nophilox": [("hpe_kernels.hip", "    const double rd = philox_u01(sw.seed, l < HPE_DOF ? ST_RP : ST_RG, g, ic, dl);",
                   "    const double rd = 0.25 + dl * 1e-3;")],
