@@ -1,4 +1,4 @@
-"""Multi-rank path on the CPU (gloo, world_size 2): the per-frame best-of-subswarms
+"""Multi-rank path on the CPU (gloo, world_size 2 and 8): the per-frame best-of-subswarms
 exchange of hpe.dist (the code bench.py runs over RCCL), with the subswarms computed by
 the C oracle so the expected winner is known independently.  SURVEY.md §8e."""
 import os
@@ -66,6 +66,17 @@ def test_exchange_picks_best_subswarm(tmp_path):
     for r in res:
         np.testing.assert_array_equal(r, expect[win])
     assert expect[0][26] != expect[1][26]  # distinct streams per rank
+
+
+def test_exchange_eight_ranks(tmp_path):
+    """The 8-GPU shape of config 5 (one subswarm per rank, seeds 1000..1007) on 8 gloo
+    ranks: every rank ends with the oracle's best of the eight subswarms."""
+    res = _run(tmp_path, "pso", world=8)
+    expect = [_subswarm(r) for r in range(8)]
+    win = int(np.argmin([e[26] for e in expect]))
+    for r in res:
+        np.testing.assert_array_equal(r, expect[win])
+    assert len({e[26] for e in expect}) == 8
 
 
 def test_exchange_tie_lowest_rank(tmp_path):
