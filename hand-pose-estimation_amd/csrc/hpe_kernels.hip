@@ -707,7 +707,6 @@ __global__ __launch_bounds__(PW_NT, WPP == 2 ? 2 : 4) void k_pso_gen_w(DevSwarm 
     // ---- round 1: every load of the generation, all independent and unconditional (the
     // push links follow once the topology is known)
     const CloudGlobal cv = obs_cloud(o);
-    const Pt pre = load_pt1(cv, l + 64 * sub);
     const size_t e = (size_t)ic * HPE_DOF + l;
     const size_t ec = (size_t)ic * HPE_DOF + (l < HPE_DOF ? l : HPE_DOF - 1);
     const double xo = sw.xh[(size_t)(g - 1) * P * HPE_DOF + ec];
@@ -772,6 +771,9 @@ __global__ __launch_bounds__(PW_NT, WPP == 2 ? 2 : 4) void k_pso_gen_w(DevSwarm 
     else wave_argmin_lex(v, idx, slot, inf, islot, XCH ? &infc : nullptr);
     const bool use_ext = XCH && readlane_f64(exr, HPE_DOF) < infc;  // strictly better
     WAVE_TS2(g, 1);
+    // the lane's first cloud point, used after FK: issued behind round 1's loads, which the
+    // informant choice waits for in issue order
+    const Pt pre = load_pt1(cv, l + 64 * sub);
     // ---- velocity, position, check_constraints (PSO.cpp:824-842, 358-377)
     if (l < HPE_DOF) {
         double vn;
