@@ -359,7 +359,6 @@ __device__ __forceinline__ void pso_gen_body(const DevSwarm &sw, const DevObs *_
         const int per = (o.n + SPLIT - 1) / SPLIT, s0 = min(slice * per, o.n);
         cv = CloudGlobal{cv.cx + s0, cv.cy + s0, cv.cz + s0, min(s0 + per, o.n) - s0};
     }
-    const Pt pre = load_pt(cv, t);  // this thread's first cloud point, used after FK
     const size_t e = (size_t)i * HPE_DOF + t;
     const int q = t - 64;  // pushing lanes (waves 1..3): var-1 links now, var-0 after the decision
     const Link lk1 = load_link(sw, g, i, q, g + 1, q < 3 * IB_FIELDS);
@@ -466,6 +465,9 @@ __device__ __forceinline__ void pso_gen_body(const DevSwarm &sw, const DevObs *_
         sc.lap(1);
     }
     hand_put<NT>(sm.hand, hw);
+    // this thread's first cloud point, used after FK: issued behind round 1's loads, which
+    // the informant choice and the row staging wait for in issue order
+    const Pt pre = load_pt(cv, t);
     BLK_TS(g, 1);
     __syncthreads();  // informant rows and draws in LDS
     SphXYZ own0{0.0, 0.0, 0.0};  // wave 0: the centres FK leaves in registers
