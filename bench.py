@@ -149,13 +149,10 @@ def extra_passes(args, ctx, lib, state, state0, raw, n_frames, P, refine, ds, wo
     import torch.distributed as dist
 
     exact0 = int(lib.hpe_get_refine_exact(ctx.h))
-    team = os.environ.get("HPE_REFINE_TEAM", "0")
     out = {"refine_form": ("chain: the reference's DH chain on every evaluation" if exact0 else
                            "hand-frame: spheres Rg q + u from centres built once per call, FK "
                            "within 1e-12 cm of the chain (DESIGN.md §2)"),
-           "refine_kernel": ("k_refine_team, leader + helper workgroups (hpe_team.hpp)" if team == "1"
-                             else "k_refine_team leader alone" if team == "solo" else
-                             "k_refine, one workgroup"),
+           "refine_kernel": "k_refine, one workgroup",
            "refine_exact_ms_per_step": None, "per_frame_graph_ms_per_step": None,
            "scaling_baseline_ms_per_step": None,
            "note": ("diagnostic passes after the timed region over the same frames (second of two "
@@ -171,7 +168,9 @@ def extra_passes(args, ctx, lib, state, state0, raw, n_frames, P, refine, ds, wo
         state.copy_(state0)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        if K2:
+        if K2 and args.resident:  # the timed loop's form: prepared frames
+            ctx.track_sequence(P, refine, state.data_ptr(), args.warmup, args.steps, K2)
+        elif K2:
             if d_raw is None:
                 d_raw = torch.from_numpy(np.ascontiguousarray(np.stack(raw), dtype=np.float32)).to(
                     f"cuda:{local}")

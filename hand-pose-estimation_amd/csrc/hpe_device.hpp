@@ -1349,13 +1349,15 @@ __device__ __forceinline__ void bf_filter_lane2(const FkSm &f, const FiltSm &fs,
 }
 // search_align_filt over points p0, p0 + step, ... U per pass (p, p + step, ...), the next
 // pass's points loaded one pass ahead; pre = the point p0.  A pass's points past the cloud
-// are evaluated at a clamped index and not added.
+// are evaluated at a clamped index and not added.  An empty cloud reads nothing (its
+// arrays may be unallocated): n is uniform, so the early return is too.
 template <int U, class CV>
 __device__ __forceinline__ double search_align_filt2(const FkSm &f, const FiltSm &fs,
                                                      const FiltC &c, const CV &cv,
                                                      const DevHand *__restrict__ H, Pt pre,
                                                      int p0, int step) {
     double acc = 0.0;
+    if (cv.n <= 0) return acc;
     const int n1 = cv.n - 1;
     Pt q[U];
     q[0] = pre;

@@ -215,79 +215,35 @@ __device__ __forceinline__ void push_inbox(const DevSwarm &sw, int g, int s, int
     push_inbox(sw, g, s, q, L.ok ? (int)(L.raw & 0xffffffff) : -1, (int)(L.raw >> 32), tt, pc, row);
 }
 
-// The split forms (SPLIT > 1, large clouds): block `slice` of particle i has summed its
-// slice of the cost into fx; its partial goes to sw.part and the last of the particle's
-// SPLIT blocks to arrive adds them in slice order (deterministic) into fx and returns
-// true; the others return false and are done.  Release: the partial stored, agent fence,
-// counter; acquire: one lane, then the barrier.
-template <int SPLIT>
-__device__ __forceinline__ bool split_arrive(const DevSwarm &sw, int g, int i, int slice,
-                                             double &fx, Smem &sm) {
-    __shared__ int last_blk;
-    if (threadIdx.x == 0) {
-        double *pp = sw.part + ((size_t)(g & 1) * sw.P + i) * SPLIT;
-        unsigned *ctr = sw.arrive + (size_t)(g & 1) * sw.P + i;
-        pp[slice] = fx;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        const unsigned prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const bool last = prev == SPLIT - 1;
-        if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            double tot = 0.0;
-#pragma unroll
-            for (int k = 0; k < SPLIT; ++k) tot += pp[k];
-            *ctr = 0u;  // next used two generations on, after kernel boundaries
-            sm.dscal[6] = tot;
-        }
-        last_blk = last ? 1 : 0;
-    }
-    __syncthreads();
-    if (!last_blk) return false;
-    fx = sm.dscal[6];
-    return true;
-}
-
-// generate_particles + the initial evaluation (PSO.cpp:56-74, 748-763).  SPLIT > 1: the
-// split form of k_pso_gen_split (the same slices and sums, so a particle's cost of the same
-// theta is the same bits in both kernels).
-template <int NT, int SPLIT, bool FILT = false>
+// generate_particles + the initial evaluation (PSO.cpp:56-74, 748-763).
+template <int NT, bool FILT = false>
 __device__ __forceinline__ void pso_init_body(const DevSwarm &sw, const double *__restrict__ x0,
                                               const DevObs *__restrict__ og,
                                               const DevHand *__restrict__ Hg) {
     const DevObs o = *og;  // the selected frame (device-resident: graph-stable args)
     __shared__ Smem sm;
-    const int P = sw.P, t = threadIdx.x;
-    const int i = SPLIT == 1 ? (int)blockIdx.x : (int)blockIdx.x % P;
-    const int slice = SPLIT == 1 ? 0 : (int)blockIdx.x / P;
+    const int t = threadIdx.x;
+    const int i = (int)blockIdx.x;
     const double hw = hand_word<NT>(Hg);
     const DevHand *__restrict__ H = &sm.hand;
     const double *sd = sw.bounds + 2 * HPE_DOF;
     // pushing lanes: waves 1..3 (q = t - 64), topology 1 = rebuilt for gen 1
     const int q = t - 64;
     const Link lk = load_link(sw, 0, i, q, 1, q < 3 * IB_FIELDS);
-    CloudGlobal cv = obs_cloud(o);
-    if (SPLIT > 1) {  // this block's slice of the cloud (as k_pso_gen_split)
-        const int per = (o.n + SPLIT - 1) / SPLIT, s0 = min(slice * per, o.n);
-        cv = CloudGlobal{cv.cx + s0, cv.cy + s0, cv.cz + s0, min(s0 + per, o.n) - s0};
-    }
+    const CloudGlobal cv = obs_cloud(o);
     const Pt pre = load_pt(cv, t);
     if (t < HPE_DOF) {  // particles = x0 + randn % std (PSO.cpp:67-72)
         const size_t e = (size_t)i * HPE_DOF + t;
         const double x = x0[t] + sw.normals[e] * sd[t];
         sm.fk.th[t] = x;
-        if (slice == 0) {
-            sw.xh[e] = x;
-            sw.pb[e] = x;
-            sw.v[e] = 0.0;
-        }
+        sw.xh[e] = x;
+        sw.pb[e] = x;
+        sw.v[e] = 0.0;
     }
-    if (sw.ext && i == 0 && slice == 0 && t == 0) sw.ext[HPE_DOF] = __builtin_inf();  // no candidate yet
+    if (sw.ext && i == 0 && t == 0) sw.ext[HPE_DOF] = __builtin_inf();  // no candidate yet
     hand_put<NT>(sm.hand, hw);
     __syncthreads();
-    double c = eval_block<EV_COST, NT, true, FILT>(sm, o, cv, H, nullptr, pre, BT_GENS, nullptr, slice == 0);
-    if constexpr (SPLIT > 1) {
-        if (!split_arrive<SPLIT>(sw, 0, i, slice, c, sm)) return;
-    }
+    const double c = eval_block<EV_COST, NT, true, FILT>(sm, o, cv, H, nullptr, pre, BT_GENS, nullptr, true);
     if (t == 0) {  // PSO.cpp:748-763; pbest costs are >= 0, so their bits order like values
         sw.pch[i] = c;
         gmin_lower(sw, 0, i, c);
@@ -298,27 +254,19 @@ __device__ __forceinline__ void pso_init_body(const DevSwarm &sw, const double *
 template <bool FILT>
 __global__ __launch_bounds__(HPE_NT) void k_pso_init(DevSwarm sw, const double *__restrict__ x0,
                                                      const DevObs *__restrict__ og, const DevHand *__restrict__ Hg) {
-    pso_init_body<HPE_NT, 1, FILT>(sw, x0, og, Hg);
+    pso_init_body<HPE_NT, FILT>(sw, x0, og, Hg);
 }
 
 // One fused generation g >= 1 (PSO.cpp:781-879).  Wave 0 carries the serial part: every
 // load of the generation at once (own state, draws, sig[g-1] / gmin[g-1], both inboxes),
 // the topology decision, the informant, the velocity step and FK, with wave-level syncs
 // only.  Waves 1..3 prefetch the push links meanwhile; then all 8 waves search.
-//
-// SPLIT > 1 (large clouds, k_pso_gen_split): SPLIT workgroups of NT threads carry one
-// particle -- blocks i, i + P, ... (the same XCD when P is a multiple of 8) -- each running
-// round 1, the velocity step and FK redundantly (the same operations on the same inputs:
-// the same bits) and searching its slice of the cloud; slice s's partial cost goes to
-// sw.part, and the last of the SPLIT to arrive (agent-scope release / acquire counter)
-// sums the partials in slice order and does pbest, gmin and the pushes.  More resident
-// waves per SIMD for a search of ~10^4 points than one 512-thread workgroup gives.
 // XCH: the opt-in per-generation exchange (sw.ext) is compiled in (k_pso_gen_x and the
 // XCH forms); the default kernels carry none of it.  ROW16: every inbox holds at most 15
 // slots (sw.K <= 15, the host's choice of instantiation): the informant argmin runs on one
 // 16-lane DPP row.  (A run-time K test left one body for both cases: the compiler no longer
 // duplicated the kernel per case, and the generation ran 0.15 us slower.)
-template <int NT, int SPLIT, bool XCH = false, bool ROW16 = true, bool FILT = false>
+template <int NT, bool XCH = false, bool ROW16 = true, bool FILT = false>
 __device__ __forceinline__ void pso_gen_body(const DevSwarm &sw, const DevObs *__restrict__ og,
                                              const DevHand *__restrict__ Hg, int g, double W1,
                                              double C1, double C2, const InboxCounts &kin) {
@@ -338,12 +286,11 @@ __device__ __forceinline__ void pso_gen_body(const DevSwarm &sw, const DevObs *_
     __shared__ Smem sm;
     __shared__ double ib[2][IB_KMAX][IB_FIELDS];
     const int P = sw.P, K = sw.K;
-    const int i = (SPLIT == 1 ? (int)blockIdx.x : (int)blockIdx.x % P) + z0, t = threadIdx.x;
-    const int slice = SPLIT == 1 ? 0 : (int)blockIdx.x / P;
+    const int i = (int)blockIdx.x + z0, t = threadIdx.x;
     // valid slots of this receiver's kept (0) / rebuilt (1) inbox: only these are read
     // (read at blockIdx.x, clamped, unconditionally: the address depends on no loaded
     // argument, so these loads leave with the argument loads instead of after them)
-    const int kb = (SPLIT == 1 ? (int)blockIdx.x : i) & (KIN_MAX - 1);
+    const int kb = (int)blockIdx.x & (KIN_MAX - 1);
     const int k0r = kin.k0[kb], k1r = kin.k1[kb];
     const int k0 = (P <= KIN_MAX) ? k0r : K, k1 = (P <= KIN_MAX) ? k1r : K;
     // Round 1: every load of the generation is issued before any value is used (one
@@ -354,11 +301,7 @@ __device__ __forceinline__ void pso_gen_body(const DevSwarm &sw, const DevObs *_
     const double hw = hand_word<NT>((const DevHand *)((const char *)Hg + z0));
     const DevHand *__restrict__ H = &sm.hand;
     sc.lap(4);
-    CloudGlobal cv = obs_cloud(o);
-    if (SPLIT > 1) {  // this block's slice of the cloud
-        const int per = (o.n + SPLIT - 1) / SPLIT, s0 = min(slice * per, o.n);
-        cv = CloudGlobal{cv.cx + s0, cv.cy + s0, cv.cz + s0, min(s0 + per, o.n) - s0};
-    }
+    const CloudGlobal cv = obs_cloud(o);
     const size_t e = (size_t)i * HPE_DOF + t;
     const int q = t - 64;  // pushing lanes (waves 1..3): var-1 links now, var-0 after the decision
     const Link lk1 = load_link(sw, g, i, q, g + 1, q < 3 * IB_FIELDS);
@@ -448,7 +391,7 @@ __device__ __forceinline__ void pso_gen_body(const DevSwarm &sw, const DevObs *_
             sg.topo = pv.topo;
         }
         if (sg.count > 0) sg.topo = g;  // topology rebuilt when count > 0 (PSO.cpp:790)
-        if (i == 0 && slice == 0 && t == 0) sw.sig[g] = sg;
+        if (i == 0 && t == 0) sw.sig[g] = sg;
         if (t == 0) {
             sm.iscal[0] = sg.topo;
             sm.dscal[4] = pci;
@@ -489,10 +432,8 @@ __device__ __forceinline__ void pso_gen_body(const DevSwarm &sw, const DevObs *_
             const double xr = xn;
             if (xr < lbt) { xn = lbt; vn = 0.; }
             if (xr > ubt) { xn = lbt; vn = 0.; }  // above max -> MIN (PSO.cpp:372)
-            if (slice == 0) {  // (every slice computes the same x, v)
-                sw.v[e] = vn;
-                sw.xh[(size_t)g * P * HPE_DOF + e] = xn;
-            }
+            sw.v[e] = vn;
+            sw.xh[(size_t)g * P * HPE_DOF + e] = xn;
             sm.fk.th[t] = xn;
             thl = xn;
         }
@@ -507,11 +448,8 @@ __device__ __forceinline__ void pso_gen_body(const DevSwarm &sw, const DevObs *_
     const double pci = sm.dscal[4];
     const Link lk0 = load_link(sw, g, i, q, topo, q >= 3 * IB_FIELDS);
     // ---- evaluation and pbest (PSO.cpp:848-861)
-    double fx = eval_block<EV_COST, NT, false, FILT>(sm, o, cv, H, nullptr, pre, g, &own0, slice == 0);
+    const double fx = eval_block<EV_COST, NT, false, FILT>(sm, o, cv, H, nullptr, pre, g, &own0, true);
     BLK_TS(g, 4);
-    if constexpr (SPLIT > 1) {
-        if (!split_arrive<SPLIT>(sw, g, i, slice, fx, sm)) return;
-    }
     sc.start();
     const bool better = fx < pci;
     const double pn = better ? fx : pci;
@@ -535,34 +473,14 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_gen(DevSwarm sw, const DevObs *_
                                                     const DevHand *__restrict__ Hg, int g,
                                                     double W1, double C1, double C2,
                                                     InboxCounts kin) {
-    pso_gen_body<HPE_NT, 1, false, ROW16, FILT>(sw, og, Hg, g, W1, C1, C2, kin);
+    pso_gen_body<HPE_NT, false, ROW16, FILT>(sw, og, Hg, g, W1, C1, C2, kin);
 }
 template <bool ROW16, bool FILT>
 __global__ __launch_bounds__(HPE_NT) void k_pso_gen_x(DevSwarm sw, const DevObs *__restrict__ og,
                                                       const DevHand *__restrict__ Hg, int g,
                                                       double W1, double C1, double C2,
                                                       InboxCounts kin) {
-    pso_gen_body<HPE_NT, 1, true, ROW16, FILT>(sw, og, Hg, g, W1, C1, C2, kin);
-}
-
-// Large clouds (N > RF_STAGE_MAX, e.g. the full ~9.3k-point cloud): SPLIT workgroups of 256
-// threads per particle, three resident per CU (<= 168 VGPRs).
-#define PSO_SPLIT 3
-#define PSO_SPLIT_NT 256
-template <int SPLIT>
-__global__ __launch_bounds__(PSO_SPLIT_NT, 3) void k_pso_init_split(DevSwarm sw,
-                                                                   const double *__restrict__ x0,
-                                                                   const DevObs *__restrict__ og,
-                                                                   const DevHand *__restrict__ Hg) {
-    pso_init_body<PSO_SPLIT_NT, SPLIT>(sw, x0, og, Hg);
-}
-template <int SPLIT, bool XCH, bool ROW16>
-__global__ __launch_bounds__(PSO_SPLIT_NT, 3) void k_pso_gen_split(DevSwarm sw,
-                                                                  const DevObs *__restrict__ og,
-                                                                  const DevHand *__restrict__ Hg,
-                                                                  int g, double W1, double C1,
-                                                                  double C2, InboxCounts kin) {
-    pso_gen_body<PSO_SPLIT_NT, SPLIT, XCH, ROW16>(sw, og, Hg, g, W1, C1, C2, kin);
+    pso_gen_body<HPE_NT, true, ROW16, FILT>(sw, og, Hg, g, W1, C1, C2, kin);
 }
 
 // ---------------------------------------------------------------- wave-per-particle form
@@ -1864,9 +1782,6 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
         atomicAdd((unsigned long long *)(evals_out + 2), (unsigned long long)evals);  // running total
     }
 }
-
-// ------------------------------------------------------------------ team refine
-#include "hpe_team.hpp"
 
 #include "hpe_optimise.hpp"
 

@@ -83,10 +83,6 @@ struct DevSwarm {
     // {pose[26], cost} of the best pbest over all subswarms at the last exchange, an extra
     // informant candidate of every particle; nullptr: off (the reference's swarm)
     double *ext;
-    // large clouds (k_pso_gen_split): slice partial costs [2][P][PSO_SPLIT] and arrival
-    // counters [2][P] by generation parity
-    double *part;
-    unsigned *arrive;
     uint64_t seed;
     int P, G, K;
 };
@@ -134,34 +130,6 @@ struct MwJob {
     int type, nnodes, pad[2];
     double th[MW_MAX_NODES][32];
 };
-// Team refine (round 5, hpe_team.hpp): workgroup 0 runs refine_init_pose on a cloud of at
-// most 256 points; TM_NH helper workgroups on its XCD serve its jobs, each with a fixed
-// task: helper h < TM_NHH evaluates the next iteration's head (correspondence cal_cost2 +
-// the six gradient points) at the h-th likeliest accepted trial point of every search, and
-// helper TM_NHH + k chunk k (8 nodes) of a complete tree of the search's next trials
-// (TM_TREE_N nodes); the leader takes whatever its walk reaches.  All hand-offs are 8-byte
-// {tag = launch epoch, value} granules (write-through, no flags, no fences): a granule is
-// valid when its tag is this launch's epoch.
-#define TM_NHH 8        // head candidates per search
-#define TM_NTH 16       // tree helpers: 8 nodes each, one per wave
-#define TM_NH (TM_NHH + TM_NTH)
-#define TM_MAXJ 256     // jobs per launch (beyond: the leader carries on alone)
-#define TM_JOB_G 96     // granules per job
-#define TM_HEAD_G 72    // granules per head result
-#define TM_TREE_N 128   // tree nodes per job (heap order from the job's bracket state)
-enum { TM_JOB_SEARCH = 1, TM_JOB_CONT = 2, TM_JOB_EXIT = 3 };
-struct DevTeam {
-    unsigned *ctl;               // [0] launch epoch (>= 1), [32] members out (last one bumps [0])
-    unsigned long long *job;     // [TM_MAXJ][TM_JOB_G] granules
-    unsigned long long *claim;   // [TM_MAXJ][32] granules: helper h has taken its task of job j
-    unsigned long long *head;    // [TM_MAXJ][TM_NHH][TM_HEAD_G] granules
-    unsigned long long *tree;    // [TM_MAXJ][TM_TREE_N][2] granules (a node cost, lo / hi)
-    int *err;                    // a claimed result never arrived (bounded wait)
-    int *err_host;
-    int nh;                      // helper workgroups in the launch (0: the leader alone)
-    int spin;
-};
-
 struct DevMw {
     MwJob *job;
     double *part;    // [MW_MAX_Q][MW_MAX_NODES] partial alignment sums

@@ -18,9 +18,12 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a gfx950 GPU (run with -m gpu)")
 
 
+@pytest.hookimpl(trylast=True)
 def pytest_collection_modifyitems(config, items):
     # torch's HIP runtime must initialise before libhpe.so's (tests that hand torch device
-    # buffers to the ABI): whenever a selected test is a GPU test, however it was selected
+    # buffers to the ABI): whenever a selected test is a GPU test, however it was selected.
+    # trylast: after pytest's own -m / -k deselection, so a CPU-only run never
+    # initialises the HIP runtime
     if any(it.get_closest_marker("gpu") for it in items):
         import torch
         torch.cuda.is_available()

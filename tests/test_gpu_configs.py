@@ -129,29 +129,6 @@ def test_config2_single_frame_256x30(oracle, ora_hand, gh, downsample):
     assert abs(c - cr) <= COST_RTOL * abs(cr)
 
 
-def test_config2_full_cloud_split_form(oracle, ora_hand, monkeypatch):
-    """The split generation form (HPE_PSO_SPLIT=1, k_pso_init_split / k_pso_gen_split: three
-    256-thread workgroups per particle, each a slice of the cloud, the partial costs summed
-    in slice order by the last to arrive) on config 2 at N = full, against the oracle with
-    exact traces -- the same decisions as the one-workgroup form."""
-    import hpe
-    monkeypatch.setenv("HPE_PSO_SPLIT", "1")
-    g2 = hpe.reference_hand(device=0)  # read at hpe_create
-    P, maxiter = 256, 31
-    poses = hand_data.trajectory(4, seed=2)
-    depth = g2.ctx.render_depth(poses[3])
-    obs = oracle.preprocess(depth, downsample=False)
-    assert obs.n > 2048
-    cf = _costfunc(g2, depth, False)
-    ub, lb, sd = oracle_np.reference_bounds()
-    pso = _pso(maxiter)
-    bestp = np.zeros(26)
-    assert pso.pso_evolve(cf, poses[2], P, bestp) == 1
-    rb, rc, tr = oracle.pso_evolve(ora_hand, obs, poses[2], P, maxiter, lb, ub, sd, seed=1000)
-    _check_pso(pso, cf, bestp, rb, rc, tr)
-    g2.ctx.close()
-
-
 def test_config4_large_swarm_4096x40(oracle, ora_hand, gh):
     """BASELINE config 4: 4096 particles x 40 generations (auto form = one wave per
     particle; informant in-degree and inbox sizes at their largest)."""

@@ -407,13 +407,56 @@ def test_edge_empty_frame_optimisers(oracle, ora_hand, gpu_hand):
     assert pso.last_gbest_cost == oc
 
 
+@pytest.mark.parametrize("form,P,wpp", [("wave", 1024, 2), ("wave", 1030, 1), ("wave", 7, 2),
+                                         ("block", 8, 0)])
+def test_edge_empty_frame_every_form(oracle, ora_hand, form, P, wpp, monkeypatch):
+    """An all-background frame (N = 0) in every generation form: the wave form at
+    one and two waves per particle (the filter search's prologue must read no point), on a
+    fresh context whose empty slot has no cloud arrays at all, and the workgroup form's
+    filter cal_cost, chosen by the cloud BOUND of a device-prepared full-cloud frame (76,800)
+    that turns out empty.  Results as the oracle's: NaN costs, gbest zeros."""
+    import ctypes as C
+
+    import hpe
+    monkeypatch.setenv("HPE_PSO_FORM", form)
+    if wpp:
+        monkeypatch.setenv("HPE_PSO_WPP", str(wpp))
+    gh = hpe.reference_hand(device=0)  # fresh context (forms read at hpe_create)
+    d = np.zeros((240, 320), np.float32)
+    obs = oracle.preprocess(d, downsample=False)
+    assert obs.n == 0
+    ub, lb, sd = oracle_np.reference_bounds()
+    pso = hpe.PSO()
+    pso.set_pso_params(ub, lb, sd, 0.7298, 1.49618, 1.49618, 3, 1e-8, 1e-8)
+    x0 = oracle_np.X0.copy()
+    rb, rc, _ = oracle.pso_evolve(ora_hand, obs, x0, P, 3, lb, ub, sd, seed=1000)
+    if form == "wave":
+        om = hpe.observedmodel(); om.set_depth_mm(d)
+        cf = hpe.costfunc(gh, om)
+        bp = np.zeros(26)
+        pso.pso_evolve(cf, x0, P, bp)
+        np.testing.assert_array_equal(bp, rb)
+        assert np.isnan(pso.last_gbest_cost) and np.isnan(rc)
+    else:  # a tracked frame on the device-prepared slot: refine + pso_evolve + cal_cost
+        ctx = gh.ctx
+        ctx.prepare_frame(1, d, True, False)
+        ctx.select_frame(1)
+        pso._push(ctx)
+        x = x0.copy(); c = C.c_double(0)
+        ctx.check(ctx.lib.hpe_track_frame(ctx.h, P, 1, hpe._lib.ptr(x, C.c_double), C.byref(c)))
+        xr, _ = oracle.refine(ora_hand, obs, x0, rigid=REFINE_RIGID)
+        rb, rc, _ = oracle.pso_evolve(ora_hand, obs, xr, P, 3, lb, ub, sd, seed=1000)
+        np.testing.assert_array_equal(x, rb)
+        assert np.isnan(c.value) and np.isnan(oracle.cal_cost(ora_hand, obs, rb))
+    gh.ctx.close()
+
+
 @pytest.mark.parametrize("P,maxiter,wpp", [(32, 11, 0), (7, 4, 0), (1, 3, 0), (1030, 3, 0),
-                                           (32, 11, 1), (1030, 3, 2), (7, 4, 2), (7, 4, 4),
-                                           (1030, 3, 4)])
+                                           (32, 11, 1), (1030, 3, 2), (7, 4, 2)])
 def test_pso_evolve_wave_form(oracle, ora_hand, np_hand, P, maxiter, wpp, monkeypatch):
     """The wave-form generation kernels (used for large swarms) against the oracle,
     including a ragged last workgroup (P not a multiple of the particles per workgroup), with
-    one, two or four waves per particle (wpp 0: the context's choice)."""
+    one or two waves per particle (wpp 0: the context's choice)."""
     import hpe
     monkeypatch.setenv("HPE_PSO_FORM", "wave")
     if wpp:
@@ -437,7 +480,7 @@ def test_pso_evolve_wave_form(oracle, ora_hand, np_hand, P, maxiter, wpp, monkey
     assert np.array_equal(cnt, tr["count"]) and np.array_equal(topo, tr["topo"])
 
 
-@pytest.mark.parametrize("wpp", [1, 2, 4])
+@pytest.mark.parametrize("wpp", [1, 2])
 def test_wave_form_cooperative_fk_bit_identical(oracle, ora_hand, np_hand, wpp, monkeypatch):
     """The wave form's workgroup-cooperative FK (fk_coop, the default) against each wave's
     own FK (HPE_FK_COOP=0), at one and two waves per particle: the same operations per item,
