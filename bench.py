@@ -13,7 +13,11 @@ N = 250 cloud points (the reference's downsample=true default; --full-cloud: all
                  (P*(G+1) per frame per rank; refine and final evaluations are not counted)
   tracked_fps  = frames per second (per rank; ranks track the same sequence)
   multi-GPU    = one process per GPU, independent subswarms (seed 1000+rank) with one
-                 RCCL all-gather of {bestp, cost} per frame; weak scaling
+                 RCCL all-gather of {bestp, cost} per frame; weak scaling.
+                 --exchange-form library (default with nccl): libhpe.so's own communicator
+                 (hpe_subswarm_init), the exchange captured into the 8-frame graphs, so N
+                 ranks run the N = 1 loop; torch: torch.distributed per frame, one graph per
+                 frame (and the gloo rehearsal)
 
 --config selects a BASELINE.json workload: seq (default; configs[1]/[2]: 256 x 30 tracked
 frames), p32 (configs[0]'s shape, 32 x 10), p4096 (configs[3], 4096 x 40), subswarm8
@@ -89,8 +93,8 @@ def parse():
                          "launch (hpe_track_raw_sequence_dev); with --resident the prepared "
                          "frames through hpe_track_sequence_dev.  0: one graph per frame "
                          "(hpe_track_pipelined from host frames / hpe_track_frame_dev).  "
-                         "Default: 8 on one GPU, 0 with N > 1 (the per-frame exchange sits "
-                         "between frames), --dump or --exchange gen:K")
+                         "Default: 8 (one GPU, or N > 1 with the library exchange), 0 with "
+                         "--exchange-form torch / gloo, --dump or --exchange gen:K")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--seed", type=int, default=TRAJ_SEED, help="trajectory seed")
@@ -102,6 +106,14 @@ def parse():
                          "(the reference's best-of-N, SURVEY.md §8e); gen:K additionally "
                          "exchanges every K generations and injects the global best as an "
                          "extra informant (ICP-PSO style, NOT the reference algorithm)")
+    ap.add_argument("--exchange-form", choices=("library", "torch"), default=None,
+                    help="N > 1: library (default with nccl) = libhpe.so's RCCL all-gather + "
+                         "pick after every frame, captured in the frame graphs "
+                         "(hpe_subswarm_init); torch = torch.distributed all_gather per frame "
+                         "between one-frame graphs (gloo always)")
+    ap.add_argument("--subswarm-world1", action="store_true",
+                    help="--gpus 1: run the library exchange on a one-rank RCCL communicator "
+                         "(the N > 1 loop's cost at N = 1; VERDICT r5 item 1)")
     ap.add_argument("--same-device", action="store_true",
                     help="every rank uses cuda:0 (rehearse N ranks on a one-GPU box; with "
                          "--backend gloo)")
@@ -114,11 +126,20 @@ def parse():
                          "as .npy under this directory")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)
     a = ap.parse_args()
+    if a.exchange_form is None:
+        a.exchange_form = "library" if a.backend == "nccl" and a.exchange == "frame" else "torch"
+    if a.exchange_form == "library" and a.backend != "nccl":
+        ap.error("--exchange-form library needs --backend nccl (RCCL)")
+    if a.subswarm_world1 and a.gpus != 1:
+        ap.error("--subswarm-world1 is the one-GPU rehearsal of the library exchange")
+    # the library exchange sits inside the frames' graphs: N ranks run the N = 1 loop
+    a.lib_exchange = (a.gpus > 1 and a.exchange_form == "library") or a.subswarm_world1
+    graphs_ok = (a.gpus == 1 or a.lib_exchange) and not a.dump
     if a.frames_per_graph is None:
-        a.frames_per_graph = 8 if (a.gpus == 1 and not a.dump and a.exchange == "frame") else 0
-    if a.frames_per_graph and not (a.gpus == 1 and not a.dump):
-        ap.error("--frames-per-graph needs one GPU and no --dump "
-                 "(the per-frame exchange / dump sit between frames)")
+        a.frames_per_graph = 8 if (graphs_ok and a.exchange == "frame") else 0
+    if a.frames_per_graph and not graphs_ok:
+        ap.error("--frames-per-graph needs one GPU or the library exchange, and no --dump "
+                 "(a per-frame torch exchange / dump sits between frames)")
     a.exchange_every = 0
     if a.exchange != "frame":
         if not a.exchange.startswith("gen:") or not a.exchange[4:].isdigit() or int(a.exchange[4:]) < 1:
@@ -140,9 +161,12 @@ def extra_passes(args, ctx, lib, state, state0, raw, n_frames, P, refine, ds, wo
       per_frame_graph_ms_per_step (N = 1) the per-frame pipelined loop of the N > 1 lines (one
                                  graph per frame, raw frames from host memory), so the driver's
                                  1 -> N curve can be read in one loop form
-      scaling_baseline_ms_per_step (N > 1) every rank tracks the frames alone in that same
-                                 per-frame loop, no exchange; the max over ranks: the N = 1
-                                 figure of this loop form on these GPUs
+      scaling_baseline_ms_per_step (N > 1) every rank tracks the frames alone, no exchange, in
+                                 the timed loop's form (the library exchange suspended:
+                                 hpe_subswarm_enable(0); the torch form: the per-frame loop);
+                                 the max over ranks: the N = 1 figure of this loop on these GPUs
+      exchange_off_ms_per_step   (--subswarm-world1) the timed loop with the library exchange
+                                 suspended: the plain N = 1 loop in the same run
     Each pass runs the frames twice (graph captures in the first) and times the second."""
     import numpy as np
     import torch
@@ -154,7 +178,7 @@ def extra_passes(args, ctx, lib, state, state0, raw, n_frames, P, refine, ds, wo
                            "within 1e-12 cm of the chain (DESIGN.md §2)"),
            "refine_kernel": "k_refine, one workgroup",
            "refine_exact_ms_per_step": None, "per_frame_graph_ms_per_step": None,
-           "scaling_baseline_ms_per_step": None,
+           "scaling_baseline_ms_per_step": None, "exchange_off_ms_per_step": None,
            "note": ("diagnostic passes after the timed region over the same frames (second of two "
                     "runs each): refine_exact = reference-order refine; per_frame_graph = one "
                     "graph per frame from host memory (the N > 1 loop form); scaling_baseline = "
@@ -191,13 +215,21 @@ def extra_passes(args, ctx, lib, state, state0, raw, n_frames, P, refine, ds, wo
         return run(K2)
 
     K = args.frames_per_graph
+    if world == 1 and args.lib_exchange:  # the same loop, the exchange suspended
+        ctx.subswarm_enable(False)
+        out["exchange_off_ms_per_step"] = twice(K)
+        ctx.subswarm_enable(True)
     ctx.check(lib.hpe_set_refine_exact(ctx.h, 1))
     out["refine_exact_ms_per_step"] = twice(K) if world == 1 else None
     ctx.check(lib.hpe_set_refine_exact(ctx.h, exact0))
     if world == 1:
         out["per_frame_graph_ms_per_step"] = twice(0)
     else:
-        ms = torch.tensor([twice(0)], dtype=torch.float64)
+        if args.lib_exchange:
+            ctx.subswarm_enable(False)
+        ms = torch.tensor([twice(K if args.lib_exchange else 0)], dtype=torch.float64)
+        if args.lib_exchange:
+            ctx.subswarm_enable(True)
         if args.backend == "nccl":
             ms = ms.to(f"cuda:{local}")
         dist.all_reduce(ms, op=dist.ReduceOp.MAX)
@@ -474,7 +506,7 @@ def main():
     import torch.distributed as dist
     import hpe
     from hpe import synth
-    from hpe.dist import GenerationExchange, exchange_best, subswarm_seed
+    from hpe.dist import GenerationExchange, exchange_best, library_exchange, subswarm_seed
 
     if args.same_device:
         local = 0
@@ -521,6 +553,8 @@ def main():
     refine = 0 if args.no_refine else 1
     gx = (GenerationExchange(ctx, args.exchange_every, args.backend)
           if args.exchange_every else None)
+    # the library's own per-frame exchange: every rank joins one RCCL communicator in libhpe.so
+    sub_info = library_exchange(ctx) if args.lib_exchange else None
 
     def step(f, ex=None):
         """One tracked frame; ex (diagnostic pass): gets the exchange's time in us."""
@@ -529,7 +563,9 @@ def main():
             ctx.check(lib.hpe_track_frame_dev(ctx.h, P, refine, C.c_void_p(state.data_ptr())))
         else:  # frame f tracked while frame f+1 is prepared inside its refine launch
             ctx.track_pipelined(P, refine, state.data_ptr(), raw[f + 1] if f + 1 < n_frames else None)
-        if world > 1 and args.backend == "nccl":
+        if args.lib_exchange:
+            pass  # the library exchanged after the frame's final kernel, on its stream
+        elif world > 1 and args.backend == "nccl":
             # best-of-N exchange on the tracker's own stream (no host sync)
             with torch.cuda.stream(ext):
                 if ex is not None:
@@ -680,7 +716,7 @@ def main():
     ctx.check(lib.hpe_refine_eval_count(ctx.h, C.byref(rev), 1))
     prof = {}
     for name, kid in (("k_pso_gen", 0), ("k_refine", 1), ("k_pso_init", 2), ("k_pso_final", 3),
-                      ("k_preprocess", 4)):
+                      ("k_preprocess", 4), ("exchange", hpe._lib.PROF_EXCHANGE)):
         nl = C.c_int32(0); tot = C.c_double(0); mn = C.c_double(0); mx = C.c_double(0)
         ctx.check(lib.hpe_profile_read_kernel(ctx.h, kid, C.byref(nl), C.byref(tot),
                                               C.byref(mn), C.byref(mx)))
@@ -688,6 +724,16 @@ def main():
                       "min_us": mn.value * 1e3, "max_us": mx.value * 1e3,
                       "total_ms": tot.value}
     ctx.check(lib.hpe_profile_enable(ctx.h, 0))
+    if args.lib_exchange:  # event pairs around the library's all-gather + pick, per frame
+        xs = {"mean": prof["exchange"]["avg_us"], "min": prof["exchange"]["min_us"],
+              "max": prof["exchange"]["max_us"], "frames": prof["exchange"]["launches"],
+              "note": ("rank 0: hipEvents around the library's RCCL all-gather + k_pick_best on "
+                       "the tracker stream (the wait for the other ranks included), in the "
+                       "direct-launch profiling pass; inside the timed graphs the same nodes run "
+                       "without the events")}
+        if ranks is not None:
+            ranks["exchange_us"] = xs
+        sub_info["exchange_us"] = xs
     extra = extra_passes(args, ctx, lib, state, state0, raw, n_frames, P, refine, ds, world, rank,
                          local)
     prof["frame_graph"] = {"launches": len(frame_us), "avg_us": sum(frame_us) / len(frame_us),
@@ -763,6 +809,13 @@ def main():
                        "cloud_points": n_pts, "refine": bool(refine),
                        "refine_form": extra["refine_form"],
                        "refine_kernel": extra["refine_kernel"],
+                       "exchange_form": (
+                           "library: libhpe.so's RCCL all-gather + k_pick_best after every "
+                           "frame, captured in the frame graphs (hpe_subswarm_init), "
+                           f"{sub_info['nranks']} rank(s)" if args.lib_exchange else
+                           "torch: torch.distributed all_gather_into_tensor + hpe_pick_best per "
+                           f"frame on the tracker stream ({args.backend})" if world > 1 else
+                           "none (one GPU)"),
                        "exchange": ("once per frame (best of N subswarms)" if not args.exchange_every
                                     else f"every {args.exchange_every} generations + per frame "
                                          "(ICP-PSO style, non-reference)"),
@@ -783,6 +836,8 @@ def main():
             "refine_exact_ms_per_step": extra["refine_exact_ms_per_step"],
             "per_frame_graph_ms_per_step": extra["per_frame_graph_ms_per_step"],
             "scaling_baseline_ms_per_step": extra["scaling_baseline_ms_per_step"],
+            "exchange_off_ms_per_step": extra["exchange_off_ms_per_step"],
+            "subswarm": sub_info,
             "extra_passes_note": extra["note"],
             "refine_evals_per_frame": rev.value / max(ref_launches, 1),
             "kernels": prof,

@@ -779,8 +779,13 @@ __global__ __launch_bounds__(HPE_NT) void k_swarm_best(DevSwarm sw, int g) {
 // on the tracker stream right after the all-gather.  Exactly hpe/dist.py pick_best
 // (torch.nan_to_num(cost, nan=inf) then the first argmin): NaN -> +inf, +inf -> the largest
 // finite double, -inf -> the lowest; ties go to the lowest rank.  One wave, world <= 64.
+// Inside a sequence (hist, cur: the library's own exchange, hpe_subswarm_init) the frame's
+// history row gets the picked state too: row *cur - 1 of the row cursor, which the frame's
+// final kernel has already advanced.
 __global__ __launch_bounds__(64) void k_pick_best(const double *__restrict__ gathered, int world,
-                                                  double *__restrict__ state) {
+                                                  double *__restrict__ state,
+                                                  double *__restrict__ hist = nullptr,
+                                                  const int *__restrict__ cur = nullptr) {
     __shared__ double cost[64];
     __shared__ int win;
     const int l = threadIdx.x;
@@ -798,7 +803,9 @@ __global__ __launch_bounds__(64) void k_pick_best(const double *__restrict__ gat
     }
     wave_sync();
     const int w = win;
-    if (l <= HPE_DOF) state[l] = gathered[(size_t)w * (HPE_DOF + 1) + l];
+    const double x = l <= HPE_DOF ? gathered[(size_t)w * (HPE_DOF + 1) + l] : 0.0;
+    if (l <= HPE_DOF) state[l] = x;
+    if (hist && cur && l <= HPE_DOF) hist[(size_t)(HPE_DOF + 1) * (cur[0] - 1) + l] = x;
 }
 
 // u64 wave helpers of k_pso_final's replay: lane l - 1's value (lane 0: fill), the

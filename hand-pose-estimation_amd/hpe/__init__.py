@@ -148,6 +148,36 @@ class Context:
             int(n), int(to_cm), int(downsample), float(focal), int(frames_per_graph),
             C.c_void_p(d_hist_ptr) if d_hist_ptr else None))
 
+    # ---- multi-GPU subswarms: the library's own per-frame exchange (hpe_subswarm_init)
+    def subswarm_init(self, uid: bytes, nranks: int, rank: int):
+        """Join the RCCL communicator named by uid (hpe.subswarm_unique_id() on rank 0, shared
+        with every rank); collective.  Every tracked frame then ends with the all-gather of
+        {bestp, cost} over the ranks and the best-of-N pick, inside the frame's graph."""
+        b = (C.c_ubyte * _lib.SUBSWARM_ID_BYTES).from_buffer_copy(bytes(uid))
+        self.check(self.lib.hpe_subswarm_init(self._h, b, int(nranks), int(rank)))
+
+    def subswarm_enable(self, on: bool):
+        self.check(self.lib.hpe_subswarm_enable(self._h, 1 if on else 0))
+
+    def subswarm_fini(self):
+        self.check(self.lib.hpe_subswarm_fini(self._h))
+
+    def subswarm_info(self, gathered=False):
+        """{"nranks", "rank", "rccl_version"[, "gathered": (nranks, 27) of the last exchange]}."""
+        n = C.c_int32(0); r = C.c_int32(0); v = C.c_int32(0)
+        self.check(self.lib.hpe_subswarm_info(self._h, C.byref(n), C.byref(r), C.byref(v), None))
+        out = {"nranks": n.value, "rank": r.value, "rccl_version": v.value}
+        if gathered and n.value:
+            g = np.zeros((n.value, 27))
+            self.check(self.lib.hpe_subswarm_info(self._h, None, None, None, ptr(g, C.c_double)))
+            out["gathered"] = g
+        return out
+
+    def graph_captures(self) -> int:
+        n = C.c_uint64(0)
+        self.check(self.lib.hpe_graph_captures(self._h, C.byref(n)))
+        return n.value
+
     def frame_readback(self, slot):
         depth = np.zeros((IMG_H, IMG_W)); dt = np.zeros((IMG_H, IMG_W), dtype=np.float32)
         cloud = np.zeros((IMG_H * IMG_W, 3)); n = C.c_int32(0)
@@ -164,6 +194,16 @@ class Context:
         self.check(self.lib.hpe_render_depth(self._h, ptr(th, C.c_double), focal,
                                              ptr(out, C.c_float)))
         return out
+
+
+def subswarm_unique_id() -> bytes:
+    """RCCL's ncclGetUniqueId (128 bytes) for hpe_subswarm_init; call on one rank."""
+    lib = _lib.load()
+    b = (C.c_ubyte * _lib.SUBSWARM_ID_BYTES)()
+    rc = lib.hpe_subswarm_unique_id(b)
+    if rc != 0:
+        raise HpeError(f"hpe_subswarm_unique_id failed ({rc}): RCCL not loadable?")
+    return bytes(b)
 
 
 def preprocess_depth(depth_mm, to_cm=True, downsample=True, focal=241.42):

@@ -8,6 +8,12 @@ Because gbest never enters the reference velocity update (PSO.cpp:824-832), exch
 once per frame is exactly "best of N independent swarms"; the winner becomes every
 rank's next-frame x0 (testmodel.cpp:138).
 
+library_exchange sets up the same per-frame exchange INSIDE libhpe.so (hpe_subswarm_init):
+the library's own RCCL communicator all-gathers and picks after every tracked frame on the
+tracker stream, captured into the tracking graphs with the frames -- so N ranks run exactly
+the N = 1 loop (8 frames per graph launch) plus one all-gather per frame.  exchange_best is
+the torch.distributed form of the same step (one graph per frame; and the gloo rehearsal).
+
 GenerationExchange adds the opt-in ICP-PSO style exchange (NOT the reference algorithm):
 every K generations each rank's best pbest is all-gathered and the best over all ranks
 becomes an extra informant candidate of every particle (hpe_set_exchange).
@@ -52,6 +58,28 @@ def exchange_best(state: torch.Tensor, gathered: torch.Tensor | None = None,
     else:
         state.copy_(pick_best(gathered.view(world, STATE_LEN)))
     return state
+
+
+def library_exchange(ctx, group=None) -> dict:
+    """Every rank of `group` (default: the world; world 1 without a process group) joins one
+    RCCL communicator owned by ctx's library: rank 0 draws the unique id, the process group
+    broadcasts it (a CUDA tensor on "nccl", a CPU one on "gloo"), then hpe_subswarm_init on
+    every rank (collective).  Returns ctx.subswarm_info()."""
+    from . import subswarm_unique_id
+    if dist.is_initialized():
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+    else:
+        world, rank = 1, 0
+    uid = subswarm_unique_id() if rank == 0 else bytes(128)
+    if world > 1:
+        dev = (torch.device("cuda", ctx.device) if dist.get_backend(group) == "nccl"
+               else torch.device("cpu"))
+        t = torch.tensor(list(uid), dtype=torch.uint8, device=dev)
+        src = dist.get_global_rank(group, 0) if group is not None else 0
+        dist.broadcast(t, src=src, group=group)
+        uid = bytes(t.cpu().tolist())
+    ctx.subswarm_init(uid, world, rank)
+    return ctx.subswarm_info()
 
 
 class GenerationExchange:

@@ -157,6 +157,33 @@ int hpe_pso_evolve(hpe_ctx *ctx, const double x0[26], int num_p, double bestp[26
  * Replaces the reference's shared gbest across its OpenMP loop (PSO.cpp:848-861). */
 int hpe_pick_best(hpe_ctx *ctx, const double *d_gathered, int world, double *d_state);
 
+/* Multi-GPU subswarms with the per-frame exchange inside the library (SURVEY.md §8e;
+ * BASELINE config 5).  One process per GPU, one context each, seed 1000 + rank
+ * (hpe_set_seed).  Rank 0 calls hpe_subswarm_unique_id and hands the 128 bytes to the other
+ * ranks (any channel, e.g. a torch.distributed broadcast); then every rank calls
+ * hpe_subswarm_init with them -- collective, RCCL's ncclCommInitRank on this context's device.
+ * From then on every tracked frame of the context (hpe_track_frame[_dev],
+ * hpe_track_pipelined, hpe_track_sequence_dev, hpe_track_raw_sequence_dev) ends with an
+ * all-gather of every rank's {bestp, cost} (27 doubles, RCCL over xGMI) and the pick of
+ * hpe_pick_best, on hpe_stream(ctx): d_state (and the frame's d_hist row) holds the best of
+ * all subswarms, which every rank tracks the next frame from (testmodel.cpp:138).  The
+ * exchange is captured into the tracking graphs with the frames, so N ranks run the N = 1
+ * loop.  Every rank must issue the same tracking calls in the same order.  nranks = 1 is
+ * allowed (RCCL copies one row).  hpe_subswarm_enable(ctx, 0) suspends the exchange (the
+ * communicator stays); hpe_subswarm_fini destroys it (hpe_destroy does too).
+ * hpe_subswarm_info: world size, rank, the RCCL version (ncclGetVersion) and, if
+ * gathered_out != NULL, a synchronous copy of the last all-gathered nranks x 27 doubles
+ * (NaN before the first exchange).  RCCL is opened at run time (librccl.so.1): without it
+ * hpe_subswarm_unique_id / _init return HPE_E_STATE and nothing else changes. */
+#define HPE_SUBSWARM_ID_BYTES 128
+int hpe_subswarm_unique_id(unsigned char id_out[HPE_SUBSWARM_ID_BYTES]);
+int hpe_subswarm_init(hpe_ctx *ctx, const unsigned char id[HPE_SUBSWARM_ID_BYTES], int nranks,
+                      int rank);
+int hpe_subswarm_enable(hpe_ctx *ctx, int on);
+int hpe_subswarm_fini(hpe_ctx *ctx);
+int hpe_subswarm_info(hpe_ctx *ctx, int32_t *nranks, int32_t *rank, int32_t *version,
+                      double *gathered_out);
+
 /* Opt-in per-generation exchange between subswarms (ICP-PSO style; NOT the reference's
  * algorithm, whose gbest never enters the velocity, PSO.cpp:824-832).  every > 0: after
  * every `every`-th generation g < maxiter-1 of each pso_evolve of this context (standalone
@@ -265,7 +292,8 @@ int hpe_track_raw_sequence_dev(hpe_ctx *ctx, int num_p, int refine, double *d_st
 #define HPE_PROF_OPT_DESCENT 5 /* k_opt_descent: pso_optimise descent phase */
 #define HPE_PROF_OPT_MOVE 6    /* k_opt_move: pso_optimise velocity / cost phase */
 #define HPE_PROF_SWARM_BEST 7 /* k_swarm_best: a subswarm's best for the per-generation exchange */
-#define HPE_PROF_KERNELS 8
+#define HPE_PROF_EXCHANGE 8   /* the per-frame subswarm exchange (RCCL all-gather + k_pick_best) */
+#define HPE_PROF_KERNELS 9
 int hpe_profile_enable(hpe_ctx *ctx, int on);
 int hpe_profile_read(hpe_ctx *ctx, int32_t *launches, double *total_ms, double *min_ms,
                      double *max_ms);

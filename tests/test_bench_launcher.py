@@ -43,10 +43,12 @@ def test_single_rank_stub():
 
 
 def test_frames_per_graph_defaults(monkeypatch):
-    """The frame loop bench.py times: on one GPU the raw frames resident in HBM, 8 frames per
-    graph (hpe_track_raw_sequence_dev); with N > 1, --dump or a per-generation exchange, one
-    graph per frame (the exchange / dump sit between frames); an explicit value wins where
-    allowed and is refused where a step sits between frames."""
+    """The frame loop bench.py times: on one GPU, and with N > 1 over the library exchange
+    (hpe_subswarm_init, the default with nccl: the all-gather inside the frames' graphs), the
+    raw frames resident in HBM, 8 frames per graph (hpe_track_raw_sequence_dev); with the torch
+    or gloo exchange, --dump or a per-generation exchange, one graph per frame (the step sits
+    between frames); an explicit value wins where allowed and is refused where a step sits
+    between frames."""
     import importlib
     import pytest
     sys.path.insert(0, str(hand_data.ROOT))
@@ -58,12 +60,20 @@ def test_frames_per_graph_defaults(monkeypatch):
 
     assert parse().frames_per_graph == 8
     assert parse("--resident").frames_per_graph == 8
-    assert parse("--gpus", "2").frames_per_graph == 0
+    assert parse("--gpus", "2").frames_per_graph == 8
+    assert parse("--gpus", "2").exchange_form == "library" and parse("--gpus", "2").lib_exchange
+    assert parse("--gpus", "2", "--exchange-form", "torch").frames_per_graph == 0
+    assert parse("--gpus", "2", "--backend", "gloo").frames_per_graph == 0
+    assert parse("--gpus", "2", "--backend", "gloo").exchange_form == "torch"
+    assert parse("--subswarm-world1").frames_per_graph == 8
+    assert parse("--subswarm-world1").lib_exchange and not parse().lib_exchange
     assert parse("--dump", "/tmp/x").frames_per_graph == 0
     assert parse("--exchange", "gen:5").frames_per_graph == 0
     assert parse("--frames-per-graph", "0").frames_per_graph == 0
     assert parse("--frames-per-graph", "4").frames_per_graph == 4
-    for bad in (("--gpus", "2", "--frames-per-graph", "8"),
+    for bad in (("--gpus", "2", "--exchange-form", "torch", "--frames-per-graph", "8"),
+                ("--gpus", "2", "--backend", "gloo", "--exchange-form", "library"),
+                ("--gpus", "2", "--subswarm-world1"),
                 ("--exchange", "gen:5", "--frames-per-graph", "8")):
         with pytest.raises(SystemExit):
             parse(*bad)

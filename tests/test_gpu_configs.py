@@ -26,7 +26,15 @@ import oracle_np
 pytestmark = pytest.mark.gpu
 
 POSE_TOL, COST_RTOL = 1e-6, 1e-8
-SEQ_POSE_TOL, SEQ_COST_RTOL = 2e-6, 1e-7  # long sequences (test_config3)
+# long sequences (test_config3), tightened to the measured values (VERDICT r5 item 2;
+# DESIGN.md §2 has the bounds and the measurements side by side).  Round 5, 400 frames:
+# pose 2.19e-7, cost 3.1e-8, drift 2.8e-7, 6-7 mismatched frames of at most 2 flips each;
+# 20 full-cloud frames: pose 5.3e-9
+SEQ_POSE_TOL, SEQ_COST_RTOL = 5e-7, 5e-8
+SEQ_DRIFT_TOL = 1e-6       # the free-running oracle's largest distance from the GPU trajectory
+SEQ_MAX_MISMATCH = 12      # refine eval-count mismatches over the 400 frames
+SEQ_MAX_FLIPS = 2          # near-tie decisions one mismatched frame may need inverted
+FULL_SEQ_POSE_TOL = 1e-7   # the 20 full-cloud frames
 # A refine whose evaluation count differs from the oracle's must have flipped a near-tie:
 # the oracle's own run from the same x0 took some decision (Goldstein test, PSO.cpp:459-474,
 # or the loop's tol > eps, :234) with a relative margin below this (a typical frame's
@@ -256,9 +264,10 @@ def test_config3_full_cloud_20_frames_pipelined(oracle, ora_hand, gh):
     print(f"{n} full-cloud frames: max |dpose| {dpose.max():.3g} (frame {int(dpose.argmax())}), "
           f"refine eval-count mismatches (frame, flipped tie's margin) {ev_mismatch}; frames "
           f"with a margin < {TIE_MARGIN:g}: {int((margin < TIE_MARGIN).sum())}")
-    assert dpose.max() <= SEQ_POSE_TOL, f"frame {int(dpose.argmax())}: pose {dpose.max()}"
-    assert len(ev_mismatch) <= max(1, n // 20)
+    assert dpose.max() <= FULL_SEQ_POSE_TOL, f"frame {int(dpose.argmax())}: pose {dpose.max()}"
+    assert len(ev_mismatch) <= 1
     assert all(m is not None for _, m in ev_mismatch), "an eval-count mismatch no near-tie explains"
+    assert all(len(m) <= SEQ_MAX_FLIPS for _, m in ev_mismatch)
 
 
 @pytest.fixture(scope="module")
@@ -304,14 +313,15 @@ def _seq400_check(oracle, ora_hand, gh, s, rigid):
           f"per-frame max |dpose| {dpose.max():.3g} (frame {int(dpose.argmax())}), max dcost "
           f"{np.nanmax(dcost):.3g}, refine eval-count mismatches {len(ev_mismatch)}, most flips a "
           f"frame needed {flips}; free-running oracle: max drift {drift.max():.3g}, first frame "
-          f"beyond {POSE_TOL:g}: {first(drift, POSE_TOL)}; mismatched frames (frame, flipped "
+          f"beyond {SEQ_DRIFT_TOL:g}: {first(drift, SEQ_DRIFT_TOL)}; mismatched frames (frame, flipped "
           f"ties (decision, margin)) {ev_mismatch}; frames with a margin < {TIE_MARGIN:g}: "
           f"{int((margin < TIE_MARGIN).sum())}, median margin {np.median(margin):.3g}")
     assert dpose.max() <= SEQ_POSE_TOL, f"frame {int(dpose.argmax())}: pose {dpose.max()}"
     assert np.all(dcost <= SEQ_COST_RTOL), f"frame {int(np.nanargmax(dcost))}: cost {dcost.max()}"
-    assert len(ev_mismatch) <= n // 20
+    assert len(ev_mismatch) <= SEQ_MAX_MISMATCH, f"{len(ev_mismatch)} mismatched frames"
     assert all(m is not None for _, m in ev_mismatch), "an eval-count mismatch no near-tie explains"
-    assert drift.max() <= 10 * SEQ_POSE_TOL, f"free-running divergence from frame {first(drift, 10 * SEQ_POSE_TOL)}"
+    assert flips <= SEQ_MAX_FLIPS, f"a mismatched frame needed {flips} flipped ties"
+    assert drift.max() <= SEQ_DRIFT_TOL, f"free-running divergence from frame {first(drift, SEQ_DRIFT_TOL)}"
 
 
 def test_config3_sequence_400_frames_pipelined(oracle, ora_hand, gh, seq400):
@@ -321,12 +331,14 @@ def test_config3_sequence_400_frames_pipelined(oracle, ora_hand, gh, seq400):
     pose (per-frame parity, no accumulated history); (2) the oracle running free over the
     whole sequence, whose largest distance from the GPU trajectory is reported.
 
-    Sequence tolerances: pose 2e-6, cost relative 1e-7 (SEQ_*).  The fp64 sums differ in
-    order (DPP tree vs Armadillo's two accumulators, ~1e-16 relative), and refine's
-    Goldstein comparisons (PSO.cpp:459-474) sit at that rounding floor once alpha * g'p is
-    ~1e-13: on ~2 % of frames a decision flips, the refine takes a few evaluations more or
-    fewer and the pose moves by up to ~1e-6 (measured on this sequence: 9 of 400 frames,
-    max 9.6e-7; free-running drift max 3.5e-7).  Each such frame must
+    Sequence tolerances (SEQ_*, at about 2x the round-5 measurements): per-frame pose 5e-7,
+    cost relative 5e-8, free-running drift 1e-6, at most 12 eval-count mismatches of at
+    most 2 flipped ties each.  The fp64 sums differ in order (DPP tree vs Armadillo's two
+    accumulators, ~1e-16 relative), and refine's Goldstein comparisons (PSO.cpp:459-474)
+    sit at that rounding floor once alpha * g'p is ~1e-13: on ~2 % of frames a decision
+    flips, the refine takes a few evaluations more or fewer and the pose moves by up to
+    ~2e-7 (round 5: 7 of 400 frames, max 1.73e-7; free-running drift 2.6e-7, DESIGN.md
+    §2).  Each such frame must
     be the oracle's refine from the same x0 with one or two near-tie decisions (relative
     margin below TIE_MARGIN) inverted: replaying the oracle with them flipped takes exactly
     the GPU's evaluation count and reaches the GPU's refined pose (_tie_replay).  Single

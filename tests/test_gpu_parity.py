@@ -414,7 +414,8 @@ def test_edge_empty_frame_every_form(oracle, ora_hand, form, P, wpp, monkeypatch
     one and two waves per particle (the filter search's prologue must read no point), on a
     fresh context whose empty slot has no cloud arrays at all, and the workgroup form's
     filter cal_cost, chosen by the cloud BOUND of a device-prepared full-cloud frame (76,800)
-    that turns out empty.  Results as the oracle's: NaN costs, gbest zeros."""
+    that turns out empty.  Results as the oracle's: NaN costs, gbest zeros and its cost 1e100
+    (PSO.cpp:739-746), the tracked frame's cal_cost(bestp) NaN."""
     import ctypes as C
 
     import hpe
@@ -436,7 +437,7 @@ def test_edge_empty_frame_every_form(oracle, ora_hand, form, P, wpp, monkeypatch
         bp = np.zeros(26)
         pso.pso_evolve(cf, x0, P, bp)
         np.testing.assert_array_equal(bp, rb)
-        assert np.isnan(pso.last_gbest_cost) and np.isnan(rc)
+        assert pso.last_gbest_cost == rc  # 1e100: no pbest ever beat the initial gbest
     else:  # a tracked frame on the device-prepared slot: refine + pso_evolve + cal_cost
         ctx = gh.ctx
         ctx.prepare_frame(1, d, True, False)

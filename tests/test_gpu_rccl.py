@@ -70,6 +70,111 @@ def test_rccl_one_rank_allgather_on_tracker_stream(tmp_path):
     print(out.stdout.strip())
 
 
+SCRIPT_LIB = r'''
+import os, sys
+import numpy as np
+import torch
+sys.path.insert(0, os.path.join(os.environ["HPE_ROOT"], "hand-pose-estimation_amd"))
+import hpe
+from hpe import synth
+from hpe.dist import library_exchange
+torch.cuda.set_device(0)
+hand = hpe.reference_hand(device=0)
+ctx = hand.ctx
+ub, lb, sd = hpe.reference_bounds()
+pso = hpe.PSO()
+P, n = 256, 16
+pso.set_pso_params(ub, lb, sd, 0.7298, 1.49618, 1.49618, 31, 1e-8, 1e-8)
+pso._push(ctx)
+poses = synth.trajectory(n + 1, 0, revert=0.02)
+raw = np.stack([np.ascontiguousarray(ctx.render_depth(th)) for th in poses]).astype(np.float32)
+d_raw = torch.from_numpy(raw).to("cuda:0")
+
+def run(fpg):
+    state = torch.zeros(27, dtype=torch.float64, device="cuda:0")
+    state[:26] = torch.from_numpy(poses[0])
+    hist = torch.zeros(n * 27, dtype=torch.float64, device="cuda:0")
+    torch.cuda.synchronize()
+    ctx.track_raw_sequence(P, 1, state.data_ptr(), d_raw.data_ptr(), n, True, True,
+                           frames_per_graph=fpg, d_hist_ptr=hist.data_ptr())
+    ctx.check(ctx.lib.hpe_sync(ctx.h))
+    return state.cpu().numpy(), hist.cpu().numpy().reshape(n, 27)
+
+def pipelined():
+    state = torch.zeros(27, dtype=torch.float64, device="cuda:0")
+    state[:26] = torch.from_numpy(poses[0])
+    torch.cuda.synchronize()
+    ctx.pipeline_begin(raw[0])
+    out = []
+    for f in range(4):
+        ctx.track_pipelined(P, 1, state.data_ptr(), raw[f + 1])
+        ctx.check(ctx.lib.hpe_sync(ctx.h))
+        out.append(state.cpu().numpy())
+    return np.array(out)
+
+plain, plain_h = run(8)
+plain_p = pipelined()
+info = library_exchange(ctx)  # world 1: no process group, the library's own communicator
+assert info["nranks"] == 1 and info["rank"] == 0 and info["rccl_version"] > 0, info
+g0 = ctx.subswarm_info(gathered=True)["gathered"]
+assert np.isnan(g0).all()  # nothing exchanged yet
+c0 = ctx.graph_captures()
+a, a_h = run(8)           # captures the chunk graphs WITH the exchange (epoch bumped)
+c1 = ctx.graph_captures()
+b, b_h = run(8)           # replays them
+c2 = ctx.graph_captures()
+assert c1 > c0 and c2 == c1, (c0, c1, c2)
+assert np.array_equal(a, plain) and np.array_equal(b, plain), (a - plain)
+assert np.array_equal(a_h, plain_h) and np.array_equal(b_h, plain_h)
+g = ctx.subswarm_info(gathered=True)["gathered"]
+assert np.array_equal(g[0], plain), (g[0], plain)  # the all-gather ran: the last frame's row
+# one graph per frame (frames_per_graph 1) and the per-frame pipelined form, with the exchange
+c, c_h = run(1)
+assert np.array_equal(c, plain) and np.array_equal(c_h, plain_h)
+assert np.array_equal(pipelined(), plain_p)
+# direct launches (profiling): one exchange event pair per frame
+ctx.check(ctx.lib.hpe_profile_enable(ctx.h, 1))
+assert np.array_equal(pipelined(), plain_p)
+import ctypes as Cc
+nl = Cc.c_int32(0); tot = Cc.c_double(0); mn = Cc.c_double(0); mx = Cc.c_double(0)
+ctx.check(ctx.lib.hpe_profile_read_kernel(ctx.h, hpe._lib.PROF_EXCHANGE, Cc.byref(nl), Cc.byref(tot),
+                                          Cc.byref(mn), Cc.byref(mx)))
+ctx.check(ctx.lib.hpe_profile_enable(ctx.h, 0))
+assert nl.value == 4, nl.value
+# suspended: the plain loop again, bit for bit
+ctx.subswarm_enable(False)
+d, d_h = run(8)
+assert np.array_equal(d, plain) and np.array_equal(d_h, plain_h)
+ctx.subswarm_enable(True)
+ctx.subswarm_fini()
+assert ctx.subswarm_info()["nranks"] == 0
+print("LIBRCCL", info["rccl_version"], "captures", c0, c1, c2, "exchange_us",
+      tot.value / max(nl.value, 1) * 1e3, "cost", plain[26])
+hand.ctx.close()
+'''
+
+
+def test_library_exchange_captured_world1(tmp_path):
+    """VERDICT r5 item 1: the library's own subswarm exchange (hpe_subswarm_init: an RCCL
+    communicator in libhpe.so; after every tracked frame an all-gather of {bestp, cost} and the
+    pick) captured INTO the raw-sequence chunk graphs, on a one-rank communicator (RCCL refuses
+    two ranks on one GPU).  The captured form must give per-frame {bestp, cost} (the history
+    rows) and the final state bit-identical to the plain N = 1 run; the replay captures
+    nothing; the all-gather really ran (the gathered row is the last frame's state, NaN before);
+    one graph per frame and the per-frame pipelined form agree too; direct launches time one
+    exchange per frame; suspending the exchange gives the plain loop again."""
+    env = dict(os.environ, HPE_ROOT=str(hand_data.ROOT))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    f = tmp_path / "librccl1.py"
+    f.write_text(SCRIPT_LIB)
+    out = subprocess.run([sys.executable, str(f)], capture_output=True, text=True, timeout=240,
+                         env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "LIBRCCL" in out.stdout, out.stdout
+    print(out.stdout.strip())
+
+
 def test_pick_best_kernel_equals_torch_pick_best():
     """hpe_pick_best (the per-frame best of N in one launch, used after the RCCL all-gather)
     against hpe.dist.pick_best on the same gathered rows: random costs, equal costs (lowest
