@@ -782,30 +782,43 @@ __global__ __launch_bounds__(HPE_NT) void k_swarm_best(DevSwarm sw, int g) {
 // Inside a sequence (hist, cur: the library's own exchange, hpe_subswarm_init) the frame's
 // history row gets the picked state too: row *cur - 1 of the row cursor, which the frame's
 // final kernel has already advanced.
+// The rule as a wave argmin (lane l = rank l; every lane gets the winner): the lexicographic
+// minimum of (sanitised cost, rank) -- rows past world carry (+inf, rank >= world), so they
+// lose to every real row, an all-NaN world included.
+__device__ __forceinline__ int pick_best_row(const double *__restrict__ gathered, int world, int l) {
+    double v = (l < world) ? gathered[(size_t)l * (HPE_DOF + 1) + HPE_DOF] : __builtin_inf();
+    if (l < world) {
+        if (v != v) v = __builtin_inf();
+        else if (v == __builtin_inf()) v = 1.7976931348623157e308;
+        else if (v == -__builtin_inf()) v = -1.7976931348623157e308;
+    }
+    int i = l;
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) {
+        const double ov = __shfl_xor(v, m);
+        const int oi = __shfl_xor(i, m);
+        if (ov < v || (ov == v && oi < i)) {
+            v = ov;
+            i = oi;
+        }
+    }
+    return __builtin_amdgcn_readfirstlane(i);
+}
+// state <- the picked row; inside a sequence the frame's history row too (row *cur - 1).
+__device__ __forceinline__ double pick_apply(const double *__restrict__ gathered, int w, int l,
+                                             double *__restrict__ state, double *__restrict__ hist,
+                                             const int *__restrict__ cur) {
+    const double x = l <= HPE_DOF ? gathered[(size_t)w * (HPE_DOF + 1) + l] : 0.0;
+    if (l <= HPE_DOF) state[l] = x;
+    if (hist && cur && l <= HPE_DOF) hist[(size_t)(HPE_DOF + 1) * (cur[0] - 1) + l] = x;
+    return x;
+}
 __global__ __launch_bounds__(64) void k_pick_best(const double *__restrict__ gathered, int world,
                                                   double *__restrict__ state,
                                                   double *__restrict__ hist = nullptr,
                                                   const int *__restrict__ cur = nullptr) {
-    __shared__ double cost[64];
-    __shared__ int win;
     const int l = threadIdx.x;
-    double v = (l < world) ? gathered[(size_t)l * (HPE_DOF + 1) + HPE_DOF] : 0.0;
-    if (v != v) v = __builtin_inf();
-    else if (v == __builtin_inf()) v = 1.7976931348623157e308;
-    else if (v == -__builtin_inf()) v = -1.7976931348623157e308;
-    cost[l] = v;
-    wave_sync();
-    if (l == 0) {
-        int w = 0;
-        for (int r = 1; r < world; ++r)
-            if (cost[r] < cost[w]) w = r;
-        win = w;
-    }
-    wave_sync();
-    const int w = win;
-    const double x = l <= HPE_DOF ? gathered[(size_t)w * (HPE_DOF + 1) + l] : 0.0;
-    if (l <= HPE_DOF) state[l] = x;
-    if (hist && cur && l <= HPE_DOF) hist[(size_t)(HPE_DOF + 1) * (cur[0] - 1) + l] = x;
+    pick_apply(gathered, pick_best_row(gathered, world, l), l, state, hist, cur);
 }
 
 // u64 wave helpers of k_pso_final's replay: lane l - 1's value (lane 0: fill), the
@@ -1545,7 +1558,7 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
                                                   const DevHand *__restrict__ Hg,
                                                   int32_t *__restrict__ match_g,
                                                   int *__restrict__ evals_out, int do_refine,
-                                                  PrepArgs pa, DevMw mw) {
+                                                  PrepArgs pa, DevMw mw, DevPick pk) {
     extern __shared__ __align__(16) unsigned char dyn[];  // staged cloud + matchId / prep
     const int nhelp = MW ? mw.Q : 0;
     if (MW && blockIdx.x >= 1 && (int)blockIdx.x <= nhelp) {
@@ -1583,7 +1596,17 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
         match = (int32_t *)(cz + o.n);
     }
     if constexpr (!STAGED) cv = obs_cloud(o);
-    if (t < HPE_DOF) rs.x0[t] = x0g[t];
+    if (pk.gath) {
+        // the previous frame's subswarm exchange: x0 = the best all-gathered state (k_pick_best's
+        // rule), also stored to d_state and the previous frame's history row
+        if (w == 0) {
+            const double x = pick_apply(pk.gath, pick_best_row(pk.gath, pk.world, l), l, x0g,
+                                        pk.hist, pk.cur);
+            if (l < HPE_DOF) rs.x0[l] = x;
+        }
+    } else if (t < HPE_DOF) {
+        rs.x0[t] = x0g[t];
+    }
     if (t == 0) rs.ts_n = 0;
     REF_TS(rs.ts_n, 0);
     __shared__ int mwflag;

@@ -130,6 +130,16 @@ struct MwJob {
     int type, nnodes, pad[2];
     double th[MW_MAX_NODES][32];
 };
+// The subswarm exchange's pick folded into the next frame's refine launch (hpe_subswarm_init,
+// inside a sequence chunk): x0 <- the best row of the all-gathered states instead of a
+// k_pick_best launch between the frames.  gath == nullptr: x0 is d_state as usual.
+struct DevPick {
+    const double *gath;  // [world][27] {bestp, cost} per rank
+    double *hist;        // the sequence's history (row *cur - 1 gets the picked state), or null
+    const int *cur;      // the row cursor
+    int world;
+};
+
 struct DevMw {
     MwJob *job;
     double *part;    // [MW_MAX_Q][MW_MAX_NODES] partial alignment sums

@@ -112,8 +112,21 @@ def pipelined():
         out.append(state.cpu().numpy())
     return np.array(out)
 
+def seq(fpg):  # the offline sequence API over device-prepared slots
+    state = torch.zeros(27, dtype=torch.float64, device="cuda:0")
+    state[:26] = torch.from_numpy(poses[0])
+    hist = torch.zeros(n * 27, dtype=torch.float64, device="cuda:0")
+    torch.cuda.synchronize()
+    ctx.track_sequence(P, 1, state.data_ptr(), 0, n, fpg, hist.data_ptr())
+    ctx.check(ctx.lib.hpe_sync(ctx.h))
+    return state.cpu().numpy(), hist.cpu().numpy().reshape(n, 27)
+
+for f in range(n):
+    ctx.prepare_frame(f, raw[f])
+ctx.check(ctx.lib.hpe_sync(ctx.h))
 plain, plain_h = run(8)
 plain_p = pipelined()
+plain_s, plain_sh = seq(8)
 info = library_exchange(ctx)  # world 1: no process group, the library's own communicator
 assert info["nranks"] == 1 and info["rank"] == 0 and info["rccl_version"] > 0, info
 g0 = ctx.subswarm_info(gathered=True)["gathered"]
@@ -127,10 +140,13 @@ assert c1 > c0 and c2 == c1, (c0, c1, c2)
 assert np.array_equal(a, plain) and np.array_equal(b, plain), (a - plain)
 assert np.array_equal(a_h, plain_h) and np.array_equal(b_h, plain_h)
 g = ctx.subswarm_info(gathered=True)["gathered"]
-assert np.array_equal(g[0], plain), (g[0], plain)  # the all-gather ran: the last frame's row
+assert np.array_equal(g[0], plain), (g[0], plain)  # this rank's row: the last frame's result
 # one graph per frame (frames_per_graph 1) and the per-frame pipelined form, with the exchange
 c, c_h = run(1)
 assert np.array_equal(c, plain) and np.array_equal(c_h, plain_h)
+for fpg in (8, 3):
+    e, e_h = seq(fpg)
+    assert np.array_equal(e, plain_s) and np.array_equal(e_h, plain_sh), fpg
 assert np.array_equal(pipelined(), plain_p)
 # direct launches (profiling): one exchange event pair per frame
 ctx.check(ctx.lib.hpe_profile_enable(ctx.h, 1))
@@ -160,9 +176,11 @@ def test_library_exchange_captured_world1(tmp_path):
     pick) captured INTO the raw-sequence chunk graphs, on a one-rank communicator (RCCL refuses
     two ranks on one GPU).  The captured form must give per-frame {bestp, cost} (the history
     rows) and the final state bit-identical to the plain N = 1 run; the replay captures
-    nothing; the all-gather really ran (the gathered row is the last frame's state, NaN before);
-    one graph per frame and the per-frame pipelined form agree too; direct launches time one
-    exchange per frame; suspending the exchange gives the plain loop again."""
+    nothing; the frame results went through the gather buffer (this rank's row is the last
+    frame's state, NaN before; the all-gather is in place, so at one rank RCCL moves nothing);
+    one graph per frame (every pick a k_pick_best launch) and the per-frame pipelined form
+    agree too; direct launches time one exchange per frame; suspending the exchange gives the
+    plain loop again."""
     env = dict(os.environ, HPE_ROOT=str(hand_data.ROOT))
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
