@@ -44,10 +44,32 @@ def _worker(rank, world, port, out_dir, mode):
     elif mode == "tie":
         st = torch.full((27,), float(rank), dtype=torch.float64)
         st[26] = 5.0
+    elif mode == "libid":
+        # hpe.dist.library_exchange's set-up on gloo ranks with a stand-in context: rank 0's
+        # unique id reaches every rank, and every rank joins with (world, its rank)
+        import hpe
+        import hpe.dist as hd
+
+        class Ctx:
+            device = 0
+
+            def subswarm_init(self, uid, nranks, rank):
+                self.args = (uid, nranks, rank)
+
+            def subswarm_info(self):
+                return {"nranks": self.args[1], "rank": self.args[2]}
+
+        uid = bytes((7 * k + 3) % 256 for k in range(128))
+        hpe.subswarm_unique_id = lambda: uid if rank == 0 else bytes(128)  # rank 0 draws
+        ctx = Ctx()
+        info = hd.library_exchange(ctx)
+        st = torch.tensor(list(ctx.args[0]) + [ctx.args[1], ctx.args[2], info["nranks"]],
+                          dtype=torch.float64)
     else:  # nan: rank 0 diverged
         st = torch.full((27,), float(rank), dtype=torch.float64)
         st[26] = float("nan") if rank == 0 else 7.0
-    exchange_best(st)
+    if mode != "libid":
+        exchange_best(st)
     np.save(os.path.join(out_dir, f"r{rank}.npy"), st.numpy())
     dist.barrier()
     dist.destroy_process_group()
@@ -94,3 +116,14 @@ def test_single_rank_is_identity():
     assert subswarm_seed(0) == 1000
     g = torch.tensor([[1.0] * 26 + [3.0], [2.0] * 26 + [3.0]], dtype=torch.float64)
     assert pick_best(g)[0] == 1.0
+
+
+def test_library_exchange_setup_broadcasts_rank0_id(tmp_path):
+    """hpe.dist.library_exchange (bench.py's N > 1 set-up of the library's own RCCL
+    communicator, hpe_subswarm_init): on 2 gloo ranks every rank receives rank 0's 128-byte
+    unique id through the process group and joins as (world 2, its own rank)."""
+    res = _run(tmp_path, "libid")
+    uid = [(7 * k + 3) % 256 for k in range(128)]
+    for r, st in enumerate(res):
+        assert list(st[:128].astype(int)) == uid
+        assert st[128] == 2 and st[129] == r and st[130] == 2
