@@ -554,6 +554,15 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
     const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
     return __hiloint2double(hi, lo);
 }
+// A value every lane of the workgroup computed identically (from the same LDS words by the
+// same operations), made provably wave-uniform for the compiler: control flow that decides
+// barriers must not look divergent to it (a barrier under divergent control flow is
+// undefined behaviour in the HIP model).  Bit-exact: every lane holds it.
+__device__ __forceinline__ double uniform_f64(double v) {
+    const int lo = __builtin_amdgcn_readfirstlane(__double2loint(v));
+    const int hi = __builtin_amdgcn_readfirstlane(__double2hiint(v));
+    return __hiloint2double(hi, lo);
+}
 __device__ __forceinline__ double row_sum16(double v) {
     v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
     v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]

@@ -905,10 +905,13 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
     }
     if (TAIL) stage_hand<HPE_NT>(sm.hand, Hg);
     // this frame's descriptor, read before the tail stages the next frame's into it (og IS
-    // seq_obs in sequence mode).  (Staging the next descriptor after the tail's
-    // own evaluation instead, behind a barrier, miscompiled with ROCm 7.2: the early returns
-    // around that evaluation no longer skipped it, and the same-eval case's gcost was
-    // overwritten by a re-evaluated cost -- tools/ab_dump.py, round 5.)
+    // seq_obs in sequence mode).  (A round-5 form staged the next descriptor after
+    // the tail's own evaluation, behind a barrier, and returned early before it on `failed`
+    // (a per-lane atomic load) and `same_eval && last >= 0` (`last` read from LDS): exits the
+    // compiler could not prove uniform, ahead of barriers -- undefined behaviour in the HIP
+    // barrier model, not a proven compiler bug.  On the box its same-eval frames came out
+    // with a re-evaluated cost (3.3e-7 relative off).  The cause was not isolated further;
+    // every such exit is now made provably uniform (readfirstlane).)
     DevObs o_early{};
     if (TAIL) o_early = *og;
     // the frame descriptor handed back at the end, loaded now (off the final chain)
@@ -994,7 +997,7 @@ __global__ __launch_bounds__(HPE_NT) void k_pso_final(DevSwarm sw, double *__res
         sm.dscal[5] = gcost;
     }
     __syncthreads();
-    last = sm.iscal[2];
+    last = __builtin_amdgcn_readfirstlane(sm.iscal[2]);  // decides the exit below (§7)
     gcost = sm.dscal[5];
     if (last >= 0 && P <= HPE_NT) {
         // one particle per thread: its pbest cost and its position row of generation
@@ -1211,7 +1214,7 @@ __device__ void mw_collect(MwLeader &ml, int *flag) {
         *flag = ok ? 1 : 0;
     }
     __syncthreads();
-    if (!*flag) ml.failed = true;
+    if (!__builtin_amdgcn_readfirstlane(*flag)) ml.failed = true;  // decides exits (§7)
 }
 
 // Node w's alignment sum: the Q partials folded by one wave in a fixed order.
@@ -1335,7 +1338,8 @@ __device__ void mw_helper(const DevMw &mw, int h, const DevObs *__restrict__ og,
             sh[1] = nn;
         }
         __syncthreads();
-        const int type = sh[0], nn = sh[1];
+        // uniform to the compiler: they decide the exit and the barriers below (§7)
+        const int type = __builtin_amdgcn_readfirstlane(sh[0]), nn = __builtin_amdgcn_readfirstlane(sh[1]);
         if (type != MW_JOB_CORR && type != MW_JOB_FROZEN) {
             // the last helper out resets the counters for the next launch
             if (type == MW_JOB_EXIT && t == 0 &&
@@ -1516,6 +1520,10 @@ __device__ __forceinline__ double gold_tree(RefineSm &rs, const DevObs &o, const
             }
         }
         if (!done && it >= 30) done = true;  // tk stays 0
+        // the round's outcome decides the next round's barriers: provably uniform (every lane
+        // walked the same LDS costs)
+        done = __builtin_amdgcn_readfirstlane(done ? 1 : 0) != 0;
+        ctx = __builtin_amdgcn_readfirstlane(ctx);
         // x0 is read only before eval_nodes' barrier in a round
         if (UPD && done && t < HPE_DOF) rs.x0[t] = rs.x0[t] - tk * gl;
         if (done && accepted >= 0) {  // keep the accepted node's spheres for the next f_k
@@ -1794,7 +1802,7 @@ __global__ __launch_bounds__(RF_NT) void k_refine(double *__restrict__ x0g, cons
             sc.lap(22);
             if (tk == 0) cnt += 1;
             // tol = sqrt(sum(grad % grad)): arrayops::accumulate (two accumulators)
-            tol = sqrt((blk == 0) ? (s0 + s2) + s1 : s1 + (s0 + s2));
+            tol = uniform_f64(sqrt((blk == 0) ? (s0 + s2) + s1 : s1 + (s0 + s2)));
             iter += 1;
             // gold_tree's last barrier published x0 and the accepted node's spheres
             base_valid = true;  // accepted node copied, or tk == 0 and x0 unchanged

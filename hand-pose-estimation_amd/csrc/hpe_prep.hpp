@@ -106,7 +106,7 @@ __device__ __forceinline__ bool prep_arrive_last(unsigned *ctr, unsigned parties
         *flag = last ? 1 : 0;
     }
     __syncthreads();
-    return *flag != 0;
+    return __builtin_amdgcn_readfirstlane(*flag) != 0;  // decides exits and barriers (§7)
 }
 
 // The same for many arriving workgroups: one counter per shard (blockIdx % ARRIVE_SHARDS,
@@ -138,7 +138,7 @@ __device__ __forceinline__ bool arrive_last_sharded(unsigned *ctr, unsigned part
         *flag = last ? 1 : 0;
     }
     __syncthreads();
-    return *flag != 0;
+    return __builtin_amdgcn_readfirstlane(*flag) != 0;  // decides exits and barriers (§7)
 }
 
 // ---- band workgroup b: rows [30b, 30b + 30)
