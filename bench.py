@@ -659,6 +659,8 @@ def main():
         el, ranks = rank_report(args, world, rank, el, final, dev, device_identity(local))
     if args.dump:
         np.save(os.path.join(args.dump, f"states_rank{rank}.npy"), np.array(dumped))
+    if sub_info is not None:  # in_graphs: the exchange ran inside the captured frame graphs
+        sub_info.update(ctx.subswarm_info())
     # per-frame device time: the same frames again with one event pair per frame on the
     # tracker stream (not in the timed region: each timing event adds a marker, ~5 us)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -810,9 +812,11 @@ def main():
                        "refine_form": extra["refine_form"],
                        "refine_kernel": extra["refine_kernel"],
                        "exchange_form": (
-                           "library: libhpe.so's RCCL all-gather + k_pick_best after every "
-                           "frame, captured in the frame graphs (hpe_subswarm_init), "
-                           f"{sub_info['nranks']} rank(s)" if args.lib_exchange else
+                           "library: libhpe.so's RCCL all-gather + pick after every frame, "
+                           + ("captured in the frame graphs" if sub_info["in_graphs"] else
+                              "direct launches (the capture fell back)")
+                           + f" (hpe_subswarm_init), {sub_info['nranks']} rank(s)"
+                           if args.lib_exchange else
                            "torch: torch.distributed all_gather_into_tensor + hpe_pick_best per "
                            f"frame on the tracker stream ({args.backend})" if world > 1 else
                            "none (one GPU)"),

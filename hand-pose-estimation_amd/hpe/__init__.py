@@ -156,20 +156,25 @@ class Context:
         b = (C.c_ubyte * _lib.SUBSWARM_ID_BYTES).from_buffer_copy(bytes(uid))
         self.check(self.lib.hpe_subswarm_init(self._h, b, int(nranks), int(rank)))
 
-    def subswarm_enable(self, on: bool):
-        self.check(self.lib.hpe_subswarm_enable(self._h, 1 if on else 0))
+    def subswarm_enable(self, on, direct=False):
+        """Suspend (False) / resume (True) the exchange; direct=True resumes it with direct
+        launches instead of captured graphs (the library's own fallback form)."""
+        self.check(self.lib.hpe_subswarm_enable(self._h, (2 if direct else 1) if on else 0))
 
     def subswarm_fini(self):
         self.check(self.lib.hpe_subswarm_fini(self._h))
 
     def subswarm_info(self, gathered=False):
-        """{"nranks", "rank", "rccl_version"[, "gathered": (nranks, 27) of the last exchange]}."""
-        n = C.c_int32(0); r = C.c_int32(0); v = C.c_int32(0)
-        self.check(self.lib.hpe_subswarm_info(self._h, C.byref(n), C.byref(r), C.byref(v), None))
-        out = {"nranks": n.value, "rank": r.value, "rccl_version": v.value}
+        """{"nranks", "rank", "rccl_version", "in_graphs"[, "gathered": (nranks, 27) rows]}."""
+        n = C.c_int32(0); r = C.c_int32(0); v = C.c_int32(0); ig = C.c_int32(0)
+        self.check(self.lib.hpe_subswarm_info(self._h, C.byref(n), C.byref(r), C.byref(v),
+                                              C.byref(ig), None))
+        out = {"nranks": n.value, "rank": r.value, "rccl_version": v.value,
+               "in_graphs": bool(ig.value)}
         if gathered and n.value:
             g = np.zeros((n.value, 27))
-            self.check(self.lib.hpe_subswarm_info(self._h, None, None, None, ptr(g, C.c_double)))
+            self.check(self.lib.hpe_subswarm_info(self._h, None, None, None, None,
+                                                  ptr(g, C.c_double)))
             out["gathered"] = g
         return out
 

@@ -75,7 +75,7 @@ SIGNATURES = {
     "hpe_subswarm_init": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int]),
     "hpe_subswarm_enable": (C.c_int, [C.c_void_p, C.c_int]),
     "hpe_subswarm_fini": (C.c_int, [C.c_void_p]),
-    "hpe_subswarm_info": (C.c_int, [C.c_void_p, ip, ip, ip, dp]),
+    "hpe_subswarm_info": (C.c_int, [C.c_void_p, ip, ip, ip, ip, dp]),
     "hpe_get_refine_exact": (C.c_int, [C.c_void_p]),
     "hpe_track_frame": (C.c_int, [C.c_void_p, C.c_int, C.c_int, dp, dp]),
     "hpe_track_frame_dev": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),

@@ -169,12 +169,16 @@ int hpe_pick_best(hpe_ctx *ctx, const double *d_gathered, int world, double *d_s
  * all subswarms, which every rank tracks the next frame from (testmodel.cpp:138).  The
  * exchange is captured into the tracking graphs with the frames, so N ranks run the N = 1
  * loop.  Every rank must issue the same tracking calls in the same order.  nranks = 1 is
- * allowed (RCCL copies one row).  hpe_subswarm_enable(ctx, 0) suspends the exchange (the
- * communicator stays); hpe_subswarm_fini destroys it (hpe_destroy does too).
- * hpe_subswarm_info: world size, rank, the RCCL version (ncclGetVersion) and, if
- * gathered_out != NULL, a synchronous copy of the last all-gathered nranks x 27 doubles
- * (NaN before the first exchange).  RCCL is opened at run time (librccl.so.1): without it
- * hpe_subswarm_unique_id / _init return HPE_E_STATE and nothing else changes. */
+ * allowed (the all-gather is in place: RCCL moves nothing).  hpe_subswarm_enable(ctx, 0)
+ * suspends the exchange (the communicator stays), 1 resumes it, 2 resumes it with every
+ * tracking call launching directly instead of through graphs -- the form the library falls
+ * back to by itself (noted once on stderr) if a capture holding the collective fails.
+ * hpe_subswarm_fini destroys the communicator (hpe_destroy does too).  hpe_subswarm_info:
+ * world size, rank, the RCCL version (ncclGetVersion), whether the exchange runs inside
+ * captured graphs (in_graphs) and, if gathered_out != NULL, a synchronous copy of the
+ * gather buffer, nranks x 27 doubles (row r = rank r's last frame result; NaN before the
+ * first).  RCCL is opened at run time (librccl.so.1): without it hpe_subswarm_unique_id /
+ * _init return HPE_E_STATE and nothing else changes.  Any output pointer may be NULL. */
 #define HPE_SUBSWARM_ID_BYTES 128
 int hpe_subswarm_unique_id(unsigned char id_out[HPE_SUBSWARM_ID_BYTES]);
 int hpe_subswarm_init(hpe_ctx *ctx, const unsigned char id[HPE_SUBSWARM_ID_BYTES], int nranks,
@@ -182,7 +186,7 @@ int hpe_subswarm_init(hpe_ctx *ctx, const unsigned char id[HPE_SUBSWARM_ID_BYTES
 int hpe_subswarm_enable(hpe_ctx *ctx, int on);
 int hpe_subswarm_fini(hpe_ctx *ctx);
 int hpe_subswarm_info(hpe_ctx *ctx, int32_t *nranks, int32_t *rank, int32_t *version,
-                      double *gathered_out);
+                      int32_t *in_graphs, double *gathered_out);
 
 /* Opt-in per-generation exchange between subswarms (ICP-PSO style; NOT the reference's
  * algorithm, whose gbest never enters the velocity, PSO.cpp:824-832).  every > 0: after

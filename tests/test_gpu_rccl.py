@@ -157,6 +157,16 @@ ctx.check(ctx.lib.hpe_profile_read_kernel(ctx.h, hpe._lib.PROF_EXCHANGE, Cc.byre
                                           Cc.byref(mn), Cc.byref(mx)))
 ctx.check(ctx.lib.hpe_profile_enable(ctx.h, 0))
 assert nl.value == 4, nl.value
+# the fallback form (exchange on, direct launches): the same bits, nothing captured
+assert ctx.subswarm_info()["in_graphs"]
+ctx.subswarm_enable(True, direct=True)
+assert not ctx.subswarm_info()["in_graphs"]
+c3 = ctx.graph_captures()
+f, f_h = run(8)
+assert np.array_equal(f, plain) and np.array_equal(f_h, plain_h)
+assert ctx.graph_captures() == c3
+ctx.subswarm_enable(True)
+assert ctx.subswarm_info()["in_graphs"]
 # suspended: the plain loop again, bit for bit
 ctx.subswarm_enable(False)
 d, d_h = run(8)
@@ -179,7 +189,8 @@ def test_library_exchange_captured_world1(tmp_path):
     nothing; the frame results went through the gather buffer (this rank's row is the last
     frame's state, NaN before; the all-gather is in place, so at one rank RCCL moves nothing);
     one graph per frame (every pick a k_pick_best launch) and the per-frame pipelined form
-    agree too; direct launches time one exchange per frame; suspending the exchange gives the
+    agree too; direct launches time one exchange per frame; the fallback form (exchange on,
+    no graphs: hpe_subswarm_enable 2) gives the same bits; suspending the exchange gives the
     plain loop again."""
     env = dict(os.environ, HPE_ROOT=str(hand_data.ROOT))
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
