@@ -204,6 +204,61 @@ def test_library_exchange_captured_world1(tmp_path):
     print(out.stdout.strip())
 
 
+SCRIPT_LIB_WAVE = r'''
+import os, sys
+import numpy as np
+import torch
+sys.path.insert(0, os.path.join(os.environ["HPE_ROOT"], "hand-pose-estimation_amd"))
+import hpe
+from hpe import synth
+from hpe.dist import library_exchange
+torch.cuda.set_device(0)
+hand = hpe.reference_hand(device=0)
+ctx = hand.ctx
+ub, lb, sd = hpe.reference_bounds()
+pso = hpe.PSO()
+P, n = 1024, 5                       # config 5's per-rank swarm: the wave form, 2 waves/particle
+pso.set_pso_params(ub, lb, sd, 0.7298, 1.49618, 1.49618, 11, 1e-8, 1e-8)
+pso.seed = 1003                      # rank 3's stream
+pso._push(ctx)
+poses = synth.trajectory(n + 1, 4, revert=0.02)
+raw = np.stack([np.ascontiguousarray(ctx.render_depth(th)) for th in poses]).astype(np.float32)
+d_raw = torch.from_numpy(raw).to("cuda:0")
+
+def run(fpg):
+    state = torch.zeros(27, dtype=torch.float64, device="cuda:0")
+    state[:26] = torch.from_numpy(poses[0])
+    hist = torch.zeros(n * 27, dtype=torch.float64, device="cuda:0")
+    torch.cuda.synchronize()
+    ctx.track_raw_sequence(P, 1, state.data_ptr(), d_raw.data_ptr(), n, True, True,
+                           frames_per_graph=fpg, d_hist_ptr=hist.data_ptr())
+    ctx.check(ctx.lib.hpe_sync(ctx.h))
+    return state.cpu().numpy(), hist.cpu().numpy().reshape(n, 27)
+
+plain, plain_h = run(8)
+library_exchange(ctx)
+for fpg in (8, 2):
+    a, a_h = run(fpg)
+    assert np.array_equal(a, plain) and np.array_equal(a_h, plain_h), fpg
+print("LIBRCCL_WAVE ok", plain[26])
+hand.ctx.close()
+'''
+
+
+def test_library_exchange_captured_world1_wave_form(tmp_path):
+    """The same one-rank check on config 5's per-rank loop (1024 particles: the wave form at
+    two waves per particle, seed 1003), chunks of 8 and 2 frames."""
+    env = dict(os.environ, HPE_ROOT=str(hand_data.ROOT))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    f = tmp_path / "librccl_wave.py"
+    f.write_text(SCRIPT_LIB_WAVE)
+    out = subprocess.run([sys.executable, str(f)], capture_output=True, text=True, timeout=240,
+                         env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "LIBRCCL_WAVE ok" in out.stdout, out.stdout
+
+
 def test_pick_best_kernel_equals_torch_pick_best():
     """hpe_pick_best (the per-frame best of N in one launch, used after the RCCL all-gather)
     against hpe.dist.pick_best on the same gathered rows: random costs, equal costs (lowest

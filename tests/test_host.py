@@ -65,6 +65,14 @@ def test_errors_fail_loudly(lib):
         assert lib.hpe_create(C.byref(h), 0, C.byref(p)) == _lib.HPE_E_NODEVICE
     assert lib.hpe_create(C.byref(h), 10 ** 6, C.byref(p)) == _lib.HPE_E_NODEVICE
     assert lib.hpe_eval_costs(None, None, 1, 0, None, None) == _lib.HPE_E_ARG
+    # the subswarm exchange's entry points (no context / no buffer: refused, nothing loaded)
+    assert lib.hpe_subswarm_unique_id(None) == _lib.HPE_E_ARG
+    idb = (C.c_ubyte * _lib.SUBSWARM_ID_BYTES)()
+    assert lib.hpe_subswarm_init(None, idb, 2, 0) == _lib.HPE_E_ARG
+    assert lib.hpe_subswarm_enable(None, 1) == _lib.HPE_E_ARG
+    assert lib.hpe_subswarm_fini(None) == _lib.HPE_E_ARG
+    assert lib.hpe_subswarm_info(None, None, None, None, None, None) == _lib.HPE_E_ARG
+    assert lib.hpe_pick_best(None, None, 2, None) == _lib.HPE_E_ARG
     import hpe
     with pytest.raises(hpe.HpeError):
         hpe.Context(p, device=10 ** 6)
