@@ -15,4 +15,8 @@ timeout -k 10 300 python bench.py --frames-per-graph 0 --no-cpu-baseline > $O/pi
 timeout -k 10 300 python bench.py --resident --frames-per-graph 0 --no-cpu-baseline > $O/resident.log 2>&1 && \
 timeout -k 10 300 python bench.py --resident --frames-per-graph 8 --no-cpu-baseline > $O/resident_seq8.log 2>&1 && \
 timeout -k 10 300 python bench.py --subswarm-world1 --no-cpu-baseline > $O/seq_subswarm_world1.log 2>&1 && \
-timeout -k 10 300 python bench.py --config subswarm8 --subswarm-world1 --no-cpu-baseline > $O/subswarm1_world1.log 2>&1
+timeout -k 10 300 python bench.py --config subswarm8 --subswarm-world1 --no-cpu-baseline > $O/subswarm1_world1.log 2>&1 && \
+timeout -k 10 300 python bench.py --config p32 --full-cloud --no-cpu-baseline > $O/p32_full.log 2>&1 && \
+timeout -k 10 300 python bench.py --config p4096 --full-cloud --steps 10 --warmup 2 --no-cpu-baseline > $O/p4096_full.log 2>&1 && \
+timeout -k 10 300 python bench.py --config subswarm8 --full-cloud --steps 10 --warmup 2 --no-cpu-baseline > $O/subswarm1_full.log 2>&1 && \
+timeout -k 10 300 python bench.py --full-cloud --steps 100 --warmup 1 --no-cpu-baseline > $O/seq100_full.log 2>&1
