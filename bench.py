@@ -158,9 +158,9 @@ def extra_passes(args, ctx, lib, state, state0, raw, n_frames, P, refine, ds, wo
     """Diagnostic passes over the timed frames, after the timed region (never in `value`):
       refine_exact_ms_per_step   the same loop with the reference-order refine (DH chain on
                                  every evaluation, hpe_set_refine_exact(1))
-      per_frame_graph_ms_per_step (N = 1) the per-frame pipelined loop of the N > 1 lines (one
-                                 graph per frame, raw frames from host memory), so the driver's
-                                 1 -> N curve can be read in one loop form
+      per_frame_graph_ms_per_step (N = 1) the per-frame pipelined loop (one graph per frame, raw
+                                 frames from host memory: the PCIe-inclusive form, and the loop
+                                 of `--exchange-form torch` lines)
       scaling_baseline_ms_per_step (N > 1) every rank tracks the frames alone, no exchange, in
                                  the timed loop's form (the library exchange suspended:
                                  hpe_subswarm_enable(0); the torch form: the per-frame loop);
@@ -181,8 +181,10 @@ def extra_passes(args, ctx, lib, state, state0, raw, n_frames, P, refine, ds, wo
            "scaling_baseline_ms_per_step": None, "exchange_off_ms_per_step": None,
            "note": ("diagnostic passes after the timed region over the same frames (second of two "
                     "runs each): refine_exact = reference-order refine; per_frame_graph = one "
-                    "graph per frame from host memory (the N > 1 loop form); scaling_baseline = "
-                    "that form on every rank alone, no exchange, max over ranks")}
+                    "graph per frame from host memory (PCIe-inclusive; the torch-exchange loop); "
+                    "scaling_baseline (N > 1) = the timed loop on every rank alone, exchange "
+                    "suspended, max over ranks; exchange_off (--subswarm-world1) = the timed loop "
+                    "with the exchange suspended")}
     if not refine:
         return out
     d_raw = None
