@@ -170,3 +170,24 @@ def test_gnd_truth_err_gpu_joints(tmp_path, oracle, ora_hand, np_hand):
     fac = [float(vals[f"gte{f}"]) for f in range(len(est))]
     np.testing.assert_allclose(fac, ref, rtol=0, atol=1e-7)
     assert fac == mirror  # same joints, same operation order
+
+
+def test_c_subswarm_exchange_world1(tmp_path, np_hand):
+    """tests/cpp/subswarm_c.c: the library's subswarm exchange driven from plain C through
+    include/hpe.h alone (INTEGRATION.md "Several GPUs"; no torch, no HIP headers): the
+    test_full loop over host frames tracked plain, on a one-rank communicator, and in the
+    exchange's direct-launch form -- every frame's {pose, cost} bit-identical."""
+    src = hand_data.ROOT / "tests" / "cpp" / "subswarm_c.c"
+    exe = tmp_path / "subswarm_c"
+    subprocess.run(["gcc", "-O1", "-std=c11", "-o", str(exe), str(src),
+                    f"-I{hand_data.ROOT / 'include'}", f"-L{PKG}", "-lhpe",
+                    f"-Wl,-rpath,{PKG}"], check=True, timeout=120)
+    poses = hand_data.trajectory(6, seed=17)
+    hand, _, _ = _write_inputs(tmp_path, np_hand, poses[:0])
+    pf = tmp_path / "poses.txt"
+    pf.write_text("\n".join(" ".join(repr(float(v)) for v in p) for p in poses) + "\n")
+    out = subprocess.run([str(exe), str(hand), str(pf), str(len(poses))], capture_output=True,
+                         text=True, timeout=240)
+    assert out.returncode == 0, (out.returncode, out.stderr[-2000:])
+    assert "subswarm_c ok" in out.stdout and "nranks=1" in out.stdout, out.stdout
+    print(out.stdout.strip())
